@@ -1,0 +1,172 @@
+/*
+ * sfmfeat.h — C-ABI of the MI355X-native feature stage (detect + describe + match)
+ * of reesque/SfmFromScratch.
+ *
+ * This is the drop-in boundary.  Every entry point replaces one reference interface;
+ * the citation after each declaration is the reference file:line it stands in for
+ * (paths relative to the reference repository root).  Plain C types only: pointers,
+ * sizes and a POD parameter struct; no torch / HIP types cross this boundary (HIP
+ * streams are passed as opaque `void*`).
+ *
+ * Error model: every function returns an int status and never aborts.
+ *   SFM_OK      0  success
+ *   SFM_EINVAL  1  bad argument          -> Python ValueError / AssertionError
+ *                                          (Runner.py:29-30, ScaleRotInvSIFT.py:38)
+ *   SFM_ESTATE  2  call out of order     -> RuntimeError (NaiveSIFT.py:49-50)
+ *   SFM_EDEVICE 3  HIP runtime failure   -> RuntimeError, text via sfm_last_error()
+ *   SFM_ERANGE  4  output capacity too small (n_out holds the required size)
+ *   SFM_EINDEX  5  matcher with fewer than 2 target descriptors -> IndexError
+ *                                          (NNRatioFeatureMatcher.py:41-43)
+ *
+ * Threading: the reference drives extractor and matcher from 8 Python threads
+ * (Runner.py:183-191).  A context is NOT shared between threads; create one context
+ * per thread (the Python wrapper keeps a thread-local context).  The library keeps no
+ * global mutable state, so distinct contexts are fully re-entrant.
+ */
+#ifndef SFMFEAT_H_
+#define SFMFEAT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SFM_OK 0
+#define SFM_EINVAL 1
+#define SFM_ESTATE 2
+#define SFM_EDEVICE 3
+#define SFM_ERANGE 4
+#define SFM_EINDEX 5
+
+/* Extractor plugin classes (FeatureExtractor/SIFT/NaiveSIFT.py, ScaleRotInvSIFT.py). */
+#define SFM_MODE_SCALEROT 0 /* ScaleRotInvSIFT: pyramid + dominant orientation */
+#define SFM_MODE_NAIVE 1    /* NaiveSIFT: one level, un-rotated descriptors */
+
+#define SFM_DESC_DIM 128
+#define SFM_MAX_GAUSS 15 /* largest gaussian_size accepted */
+#define SFM_MAX_KSIZE 31 /* largest NMS ksize accepted */
+#define SFM_MAX_FW 64    /* largest feature_width accepted */
+#define SFM_MAX_LEVELS 12
+
+/*
+ * POD mirror of the reference's `extractor_params` dict keys.  Defaults are the
+ * reference's `.get(key, default)` values:
+ *   num_interest_points 2500  FeatureExtractor.py:11
+ *   ksize 7, gaussian_size 7, sigma 5, alpha 0.05, feature_width 16  NaiveSIFT.py:35-39
+ *   pyramid_level 4, pyramid_scale_factor 2                          ScaleRotInvSIFT.py:12-13
+ * `gauss_kernel` optionally carries the float32 values of
+ * NaiveSIFT._generate_gaussian_kernel (NaiveSIFT.py:175-199) computed by the caller
+ * (the Python wrapper computes them with numpy exactly as the reference does); when
+ * `gauss_kernel_set` is 0 the library computes them itself in double precision.
+ */
+typedef struct sfm_params {
+  int32_t mode;
+  int32_t num_interest_points;
+  int32_t ksize;
+  int32_t gaussian_size;
+  int32_t feature_width;
+  int32_t pyramid_level;
+  double sigma;
+  double alpha;
+  double pyramid_scale_factor;
+  int32_t gauss_kernel_set;
+  int32_t reserved0;
+  float gauss_kernel[SFM_MAX_GAUSS * SFM_MAX_GAUSS];
+} sfm_params;
+
+/* Fill `p` with the reference defaults for `mode`. */
+void sfm_params_default(sfm_params* p, int32_t mode);
+
+/* ABI version, bumped on any signature change. */
+int32_t sfm_abi_version(void);
+
+/* Maximum number of keypoints one image can produce:
+ * ScaleRot: pyramid_level * int(k / pyramid_level)  (ScaleRotInvSIFT.py:90 scaled_k)
+ * Naive:    k                                       (NaiveSIFT.py:100-103) */
+int64_t sfm_keypoint_capacity(const sfm_params* p);
+
+/* Pyramid level sizes for an H x W image, chained int(w/s), int(h/s)
+ * (ScaleRotInvSIFT.py:109-115).  dims receives 2*L ints (h0,w0,h1,w1,...). */
+int32_t sfm_pyramid_dims(const sfm_params* p, int32_t H, int32_t W, int32_t* dims);
+
+typedef struct sfm_ctx sfm_ctx;
+
+/* Create a context bound to HIP device `device` with fixed extractor parameters. */
+int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out);
+int32_t sfm_ctx_destroy(sfm_ctx* ctx);
+/* Last error text for this context (never NULL). */
+const char* sfm_last_error(const sfm_ctx* ctx);
+
+/*
+ * Per-image extraction from host memory — replaces the ScaleRotInvSIFT constructor
+ * (ScaleRotInvSIFT.py:9-16, all work eager) and NaiveSIFT.detect_keypoints +
+ * extract_descriptors (NaiveSIFT.py:42-52), chosen by params.mode.
+ *   img: H x W float32 grayscale, row stride `row_stride` elements (>= W)
+ *   X, Y: int64 column / row of each keypoint in level-0 pixels
+ *         (ScaleRotInvSIFT.py:101-102: (x * s^l).astype(int))
+ *   desc: n x 128 float32 RootSIFT descriptors (ScaleRotInvSIFT.py:79-85)
+ *   cap: capacity of X/Y/desc in keypoints; n_out: keypoints written
+ *   level_counts: optional, pyramid_level ints — keypoints contributed per level
+ *                 (the Python wrapper uses it to mirror ScaleRotInvSIFT.py:103's
+ *                 ragged extend when a level yields exactly one keypoint)
+ * Output order is the reference's: level by level, confidence descending.
+ */
+int32_t sfm_extract(sfm_ctx* ctx, const float* img, int32_t H, int32_t W, int64_t row_stride,
+                    int64_t* X, int64_t* Y, float* desc, int64_t cap, int64_t* n_out,
+                    int32_t* level_counts);
+
+/*
+ * Brute-force L2 nearest neighbour with Lowe ratio test — replaces
+ * NNRatioFeatureMatcher.match_features_ratio_test (NNRatioFeatureMatcher.py:8-60).
+ *   d1: n1 x 128, d2: n2 x 128 float32 (row-major, contiguous)
+ *   ratio: threshold, compared in float32 (`nndr <= float32(ratio)`, :49)
+ *   matches: k x 2 int64 [row in d1, row in d2]; conf: k float32 nndr
+ *   sorted by (conf ascending, row ascending).  cap >= n1 always suffices.
+ * Returns SFM_EINDEX when n2 < 2 (the reference raises IndexError at :42).
+ */
+int32_t sfm_match(sfm_ctx* ctx, const float* d1, int64_t n1, const float* d2, int64_t n2,
+                  float ratio, int64_t* matches, float* conf, int64_t cap, int64_t* k_out);
+
+/* ---------------- device-resident batch API (throughput path) ----------------
+ * All pointers are device pointers on the context's device; `stream` is a
+ * hipStream_t (NULL = the context's own stream).  The calls are asynchronous with
+ * respect to the host: results are valid once the stream has been synchronised.
+ * Workspace is owned by the context; call sfm_reserve() once with the largest batch
+ * so that the batch calls perform no device allocation (hipGraph-capturable).
+ *
+ * Slot table layout (also the RCCL all-gather unit):
+ *   xy    [B][cap][2] int32   (X, Y) level-0 pixel coordinates
+ *   desc  [B][cap][128] float32
+ *   count [B] int32
+ */
+int32_t sfm_reserve(sfm_ctx* ctx, int32_t B, int32_t H, int32_t W);
+
+/* Extract B images of identical size H x W stored contiguously ([B][H][W] float32). */
+int32_t sfm_extract_batch_dev(sfm_ctx* ctx, const float* imgs, int32_t B, int32_t H, int32_t W,
+                              int32_t* xy, float* desc, int32_t* count, int64_t cap,
+                              void* stream);
+
+/* Same, from 8-bit grayscale frames ([B][H][W] uint8, value/255 as float32 —
+ * the conversion of Runner.py:507-509,521 done on the device). */
+int32_t sfm_extract_batch_u8_dev(sfm_ctx* ctx, const uint8_t* imgs, int32_t B, int32_t H,
+                                 int32_t W, int32_t* xy, float* desc, int32_t* count,
+                                 int64_t cap, void* stream);
+
+/*
+ * Match P image pairs out of a slot table (the consecutive / all-pairs schedule of
+ * Runner.py:183-191).  pairs: [P][2] int32 image indices into the slot table.
+ * Output per pair p: matches [p][cap][2] int32 (row in first, row in second),
+ * conf [p][cap] float32, nmatch [p] int32; sorted as sfm_match.  A pair whose second
+ * image has fewer than 2 keypoints yields nmatch = -1 (the reference's IndexError).
+ */
+int32_t sfm_match_pairs_dev(sfm_ctx* ctx, const float* desc, const int32_t* count, int64_t cap,
+                            const int32_t* pairs, int32_t P, float ratio, int32_t* matches,
+                            float* conf, int32_t* nmatch, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SFMFEAT_H_ */
