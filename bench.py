@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""bench.py — images/sec detect+describe+match at 1080p on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): per GPU, a batch of 32 synthetic 1080p frames
+(uint8 -> float32 gray, device-resident before timing), ScaleRotInvSIFT with the
+"octave" parameters (4 levels x 2, k 2500, ksize 3, 7x7 Gaussian sigma 6, alpha 0.05,
+feature width 18), then NNRatioFeatureMatcher(0.85) over consecutive pairs — the
+reference's schedule (Runner.py:183).  One step = extract the batch + match its pairs.
+
+Multi-GPU (weak scaling, one process per GPU, torchrun): rank r owns frames
+[r*B, (r+1)*B) of one global sequence.  The only exchange is the reference's consecutive
+pair that straddles two shards: the first slot of every rank's descriptor table is
+all-gathered over RCCL and rank r also matches (its last frame, rank r+1's first frame).
+
+Prints ONE JSON line (rank 0) with the driver's contract fields plus `roofline`
+(dominant kernel, live HIP-event timing inside the timed region) and `cpu_baseline`
+(the C restatement in oracle/, timed on a bounded sample on this host, rank 0, N=1).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+P_OCT = {"num_interest_points": 2500, "ksize": 3, "gaussian_size": 7, "sigma": 6, "alpha": 0.05,
+         "feature_width": 18, "pyramid_level": 4, "pyramid_scale_factor": 2}
+RATIO = 0.85
+H, W = 1080, 1920
+PEAK_F32_TFLOPS = 157.3   # MI355X FP32 (vector == matrix) dense peak, MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0     # HBM3E spec
+
+# algorithmic work per pixel / per pair
+HARRIS_FLOP_PER_PX = 328   # Sobel 2x6 fma (24) + 3 products + 3x49 fma (294) + R (7)
+HARRIS_BYTES_PER_PX = 8    # read the level once, write R once
+MATCH_FLOP_PER_ELEM = 3    # (a-b), square, accumulate: separately rounded f32 ops
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(sample_frames: int):
+    """The C oracle (scalar restatement, 1 thread) on `sample_frames` 1080p frames and
+    their consecutive pairs; returns images/s."""
+    from oracle import oracle as O
+    from sfmfromscratch_amd import synth
+    imgs = [synth.make_frame(H, W, 1234, i) for i in range(sample_frames)]
+    t0 = time.perf_counter()
+    descs = [O.extract(im, P_OCT)[2] for im in imgs]
+    for i in range(sample_frames - 1):
+        O.match(descs[i], descs[i + 1], RATIO)
+    dt = time.perf_counter() - t0
+    return sample_frames / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
+    ap.add_argument("--cpu-sample", type=int, default=4, help="frames in the CPU baseline sample (0 = skip)")
+    ap.add_argument("--no-profile", action="store_true", help="disable the live per-stage HIP events")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from sfmfromscratch_amd import synth
+    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, SlotTable, consecutive_pairs
+
+    B = args.batch
+    ex = BatchExtractor(P_OCT, device=local)
+    cap = ex.cap
+    ex.reserve(B, H, W)
+    matcher = BatchMatcher(RATIO, device=local, ctx=ex.ctx)
+
+    # device-resident float32 frames of this rank's shard of the global sequence
+    frames_u8 = np.stack([synth.make_frame_u8(H, W, 1234, rank * B + i) for i in range(B)])
+    frames = torch.from_numpy(synth.u8_to_gray(frames_u8)).to(dev)
+    del frames_u8
+    slots = SlotTable(torch, B + 1, cap, dev)           # slot B = neighbour's first frame (halo)
+    has_next = rank < world - 1
+    pairs_np = consecutive_pairs(B)
+    if has_next:
+        pairs_np = np.concatenate([pairs_np, np.array([[B - 1, B]], np.int32)])
+    pairs = torch.from_numpy(pairs_np).to(dev)
+    P = pairs.shape[0]
+    mout = (torch.zeros((P, cap, 2), dtype=torch.int32, device=dev),
+            torch.zeros((P, cap), dtype=torch.float32, device=dev),
+            torch.zeros((P,), dtype=torch.int32, device=dev))
+    gath_desc = torch.zeros((world, cap, 128), dtype=torch.float32, device=dev) if world > 1 else None
+    gath_cnt = torch.zeros((world,), dtype=torch.int32, device=dev) if world > 1 else None
+
+    class View:  # the first B rows of the slot table, as the extractor's output
+        xy, desc, count = slots.xy[:B], slots.desc[:B], slots.count[:B]
+
+    def step():
+        ex.extract(frames, out=View)
+        if world > 1:
+            dist.all_gather_into_tensor(gath_desc, slots.desc[0].contiguous())
+            dist.all_gather_into_tensor(gath_cnt, slots.count[0:1].contiguous())
+            if has_next:
+                slots.desc[B].copy_(gath_desc[rank + 1])
+                slots.count[B:B + 1].copy_(gath_cnt[rank + 1:rank + 2])
+        matcher.match(slots, pairs, out=mout)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if not args.no_profile:
+        ex.ctx.profile_enable(True)
+        ex.ctx.profile_read(reset=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    elapsed = max(wall, gpu_ms / 1e3)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    prof = ex.ctx.profile_read(reset=True) if not args.no_profile else {}
+    counts = slots.count.cpu().numpy()
+    nmatch = mout[2].cpu().numpy()
+
+    images = world * B * args.steps
+    value = images / elapsed
+    roof = None
+    stages = {}
+    if prof:
+        # algorithmic work in the timed region
+        levels = [(H >> l, W >> l) for l in range(P_OCT["pyramid_level"])]
+        px = sum(h * w for h, w in levels) * B * args.steps
+        pair_elems = sum(int(counts[i]) * int(counts[j]) for i, j in pairs_np) * 128 * args.steps
+        work = {
+            "harris": ("mfma", HARRIS_FLOP_PER_PX * px / 1e12, "TFLOP/s", PEAK_F32_TFLOPS,
+                       HARRIS_BYTES_PER_PX * px),
+            "match": ("mfma", MATCH_FLOP_PER_ELEM * pair_elems / 1e12, "TFLOP/s", PEAK_F32_TFLOPS, None),
+        }
+        stages = {k: {"ms_total": round(v[0], 3), "launches": v[1]} for k, v in prof.items() if v[1]}
+        dom = max(prof, key=lambda k: prof[k][0])
+        if dom in work:
+            bound, amount, unit, peak, _ = work[dom]
+            ms, n = prof[dom]
+            achieved = amount / (ms / 1e3)
+            roof = {"kernel": {"harris": "k_harris<7>", "match": "k_match_rows"}[dom], "bound": bound,
+                    "achieved": round(achieved, 3), "peak": peak, "unit": unit,
+                    "frac": round(achieved / peak, 4), "traffic": None,
+                    "avg_launch_ms": round(ms / max(n, 1), 4), "launches": n}
+        else:
+            roof = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": None, "traffic": None}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        v, dt = cpu_baseline(args.cpu_sample)
+        cpu = {"value": round(v, 4), "unit": "images/sec", "cores": 1, "kind": "port",
+               "sample": f"oracle/sfm_oracle.c (C restatement, 1 thread) on {args.cpu_sample} synthetic "
+                         f"1080p frames + {args.cpu_sample - 1} consecutive pairs, {dt:.1f} s"}
+
+    if rank == 0:
+        out = {
+            "metric": "images/sec detect+describe+match, 1080p, 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic integer-generated textured 1080p frames, device-resident f32)",
+            "config": {"workload": "BASELINE configs[1]: 32x 1080p per GPU, ScaleRotInvSIFT 4-level x2 octave "
+                                   "pyramid, k=2500, fw 18, NNRatio 0.85 over consecutive pairs",
+                       "frames_per_gpu": B, "image": [H, W], "pairs_per_gpu": int(P),
+                       "keypoints_mean": float(np.mean(counts[:B])),
+                       "matches_mean": float(np.mean(nmatch[nmatch >= 0])) if (nmatch >= 0).any() else 0.0,
+                       "parallelism": f"image-shard x{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "stages_ms": stages,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

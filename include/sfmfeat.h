@@ -107,6 +107,7 @@ const char* sfm_last_error(const sfm_ctx* ctx);
  *   X, Y: int64 column / row of each keypoint in level-0 pixels
  *         (ScaleRotInvSIFT.py:101-102: (x * s^l).astype(int))
  *   desc: n x 128 float32 RootSIFT descriptors (ScaleRotInvSIFT.py:79-85)
+ *   conf: optional, n float32 Harris responses (NaiveSIFT.py:44 `self.confidences`)
  *   cap: capacity of X/Y/desc in keypoints; n_out: keypoints written
  *   level_counts: optional, pyramid_level ints — keypoints contributed per level
  *                 (the Python wrapper uses it to mirror ScaleRotInvSIFT.py:103's
@@ -114,8 +115,8 @@ const char* sfm_last_error(const sfm_ctx* ctx);
  * Output order is the reference's: level by level, confidence descending.
  */
 int32_t sfm_extract(sfm_ctx* ctx, const float* img, int32_t H, int32_t W, int64_t row_stride,
-                    int64_t* X, int64_t* Y, float* desc, int64_t cap, int64_t* n_out,
-                    int32_t* level_counts);
+                    int64_t* X, int64_t* Y, float* desc, float* conf, int64_t cap,
+                    int64_t* n_out, int32_t* level_counts);
 
 /*
  * Brute-force L2 nearest neighbour with Lowe ratio test — replaces
@@ -155,15 +156,41 @@ int32_t sfm_extract_batch_u8_dev(sfm_ctx* ctx, const uint8_t* imgs, int32_t B, i
                                  int64_t cap, void* stream);
 
 /*
- * Match P image pairs out of a slot table (the consecutive / all-pairs schedule of
- * Runner.py:183-191).  pairs: [P][2] int32 image indices into the slot table.
+ * Match P image pairs out of a slot table of `nimg` images (the consecutive / all-pairs
+ * schedule of Runner.py:183-191).  pairs: [P][2] int32 image indices into the table.
  * Output per pair p: matches [p][cap][2] int32 (row in first, row in second),
  * conf [p][cap] float32, nmatch [p] int32; sorted as sfm_match.  A pair whose second
  * image has fewer than 2 keypoints yields nmatch = -1 (the reference's IndexError).
  */
-int32_t sfm_match_pairs_dev(sfm_ctx* ctx, const float* desc, const int32_t* count, int64_t cap,
-                            const int32_t* pairs, int32_t P, float ratio, int32_t* matches,
-                            float* conf, int32_t* nmatch, void* stream);
+int32_t sfm_match_pairs_dev(sfm_ctx* ctx, const float* desc, const int32_t* count, int32_t nimg,
+                            int64_t cap, const int32_t* pairs, int32_t P, float ratio,
+                            int32_t* matches, float* conf, int32_t* nmatch, void* stream);
+
+/* ---------------- stage profiling (bench.py's live roofline numbers) ----------------
+ * When enabled, every stage's launches are bracketed by HIP events on the launch
+ * stream; sfm_profile_read synchronises them and returns the accumulated device time
+ * (ms) and bracket count per stage, indexed by SFM_PROF_*. */
+#define SFM_PROF_PYRAMID 0
+#define SFM_PROF_HARRIS 1
+#define SFM_PROF_MEDIAN 2
+#define SFM_PROF_NMS 3
+#define SFM_PROF_TOPK 4
+#define SFM_PROF_DESCRIBE 5
+#define SFM_PROF_MATCH_PREP 6
+#define SFM_PROF_MATCH 7
+#define SFM_PROF_MATCH_POST 8
+#define SFM_PROF_STAGES 9
+int32_t sfm_profile_enable(sfm_ctx* ctx, int32_t on);
+int32_t sfm_profile_read(sfm_ctx* ctx, double* ms, int64_t* launches, int32_t reset);
+
+/* ---------------- diagnostics (used by the parity tests) ----------------
+ * Run individual stages of the same device code on host data. */
+/* numpy-SVML-exact float32 atan2 on the device (np.arctan2, ScaleRotInvSIFT.py:42). */
+int32_t sfm_debug_atan2(int32_t device, const float* y, const float* x, float* out, int64_t n);
+/* Harris R map, exact median and candidate count of one plane (NaiveSIFT.py:59-97). */
+int32_t sfm_debug_harris(int32_t device, const float* gauss, int32_t gs, double alpha,
+                         int32_t ksize, const float* img, int32_t H, int32_t W, float* R_out,
+                         float* median_out, int64_t* ncand_out);
 
 #ifdef __cplusplus
 }

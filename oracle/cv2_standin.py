@@ -8,8 +8,10 @@ golden vectors.  The rules below are the ones oracle/sfm_oracle.c and the HIP ke
 implement; parity with real OpenCV is UNPINNED for these two calls.
 
 filter2D  (NaiveSIFT.py:67-69, 212-213): correlation, anchor at the kernel centre,
-          BORDER_CONSTANT zeros, float32 kernel; acc = +0, then acc = acc + k*p for every
-          non-zero tap in row-major kernel order, multiply and add rounded separately.
+          BORDER_CONSTANT zeros, float32 kernel; acc = +0, then acc = fma(k, p, acc) for
+          every non-zero tap in row-major kernel order (OpenCV's FilterVec_32f v_muladd
+          chain).  numpy has no fused multiply-add, so this delegates to the C oracle's
+          orc_filter2d (fmaf), the same restatement the oracle and the HIP kernels use.
 resize    (ScaleRotInvSIFT.py:114), INTER_LINEAR on float32: exact 2x downscale uses
           OpenCV's INTER_AREA-fast switch ((a00+a01)+(a10+a11))*0.25; otherwise
           half-pixel bilinear with OpenCV's coefficient rule (see _coeffs).
@@ -28,20 +30,9 @@ def filter2D(src, ddepth, kernel, dst=None, anchor=None, delta=0, borderType=BOR
         raise TypeError("cv2 stand-in: filter2D supports 2-D float32 only")
     if ddepth != -1 or borderType != BORDER_CONSTANT or delta != 0:
         raise TypeError("cv2 stand-in: only ddepth=-1, BORDER_CONSTANT, delta=0")
+    from oracle import oracle as _orc  # C restatement with fmaf
     k = np.asarray(kernel).astype(np.float32)
-    kh, kw = k.shape
-    ay, ax = kh // 2, kw // 2
-    H, W = src.shape
-    pad = np.zeros((H + kh - 1, W + kw - 1), np.float32)
-    pad[ay:ay + H, ax:ax + W] = src
-    acc = np.zeros((H, W), np.float32)
-    for i in range(kh):
-        for j in range(kw):
-            kv = k[i, j]
-            if kv == 0:
-                continue
-            acc = acc + kv * pad[i:i + H, j:j + W]
-    return acc
+    return _orc.filter2d(np.ascontiguousarray(src), k)
 
 
 def _coeffs(dn: int, sn: int):

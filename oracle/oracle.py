@@ -52,7 +52,7 @@ def lib():
         L.orc_descriptors.argtypes = [_fp, ctypes.c_int, ctypes.c_int, _i64p, _i64p, ctypes.c_long,
                                       ctypes.c_int, ctypes.c_int, _fp]
         L.orc_extract.argtypes = [_fp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(SfmParams), _i64p, _i64p,
-                                  _fp, ctypes.c_long, _i32p]
+                                  _fp, _fp, ctypes.c_long, _i32p]
         L.orc_extract.restype = ctypes.c_long
         L.orc_match.argtypes = [_fp, ctypes.c_long, _fp, ctypes.c_long, ctypes.c_float, _i64p, _fp]
         L.orc_match.restype = ctypes.c_long
@@ -158,8 +158,9 @@ def descriptors(img, X, Y, fw: int, rotate: bool):
     return out[: len(X)]
 
 
-def extract(img, params: dict | None = None, mode: int = SFM_MODE_SCALEROT):
-    """Whole extractor: returns X, Y (int64), desc (N,128) float32, level_counts."""
+def extract(img, params: dict | None = None, mode: int = SFM_MODE_SCALEROT, with_conf: bool = False):
+    """Whole extractor: returns X, Y (int64), desc (N,128) float32, level_counts
+    (+ per-keypoint Harris confidences when with_conf)."""
     p = params_from_dict(params, mode)
     img = _c32(img)
     cap = max(keypoint_capacity(p), 1)
@@ -167,10 +168,13 @@ def extract(img, params: dict | None = None, mode: int = SFM_MODE_SCALEROT):
     Y = np.zeros(cap, np.int64)
     D = np.zeros((cap, 128), np.float32)
     lc = np.zeros(max(p.pyramid_level, 1), np.int32)
+    C = np.zeros(cap, np.float32)
     n = lib().orc_extract(_f(img), img.shape[0], img.shape[1], ctypes.byref(p), X.ctypes.data_as(_i64p),
-                          Y.ctypes.data_as(_i64p), _f(D), cap, lc.ctypes.data_as(_i32p))
+                          Y.ctypes.data_as(_i64p), _f(D), _f(C), cap, lc.ctypes.data_as(_i32p))
     if n < 0:
         raise ValueError(f"oracle extract failed: {-n}")
+    if with_conf:
+        return X[:n], Y[:n], D[:n], lc, C[:n]
     return X[:n], Y[:n], D[:n], lc
 
 

@@ -83,8 +83,11 @@ ORC_API int orc_gaussian_kernel(int ks, double sigma, float* out) {
 /* ------------------------------------------------------------------------------- */
 /* cv2.filter2D(src, -1, kernel, borderType=BORDER_CONSTANT) restated               */
 /* (call sites NaiveSIFT.py:67-69, 212-213): correlation, anchor at the kernel       */
-/* centre, zero border.  acc starts at +0 and adds k*p for every NON-ZERO tap in     */
-/* row-major kernel order, multiply and add rounded separately.                      */
+/* centre, zero border.  acc starts at +0 and acc = fmaf(k, p, acc) for every NON-ZERO*/
+/* tap in row-major kernel order — OpenCV's own float path (FilterVec_32f:           */
+/* s = v_muladd(src, k, s) over preprocess2DKernel's row-major non-zero taps, FMA    */
+/* under its AVX2 dispatch).  For the Sobel taps (+-1, +-2) k*p is exact, so the     */
+/* gradients equal the unfused sum bit for bit.                                      */
 /* ------------------------------------------------------------------------------- */
 ORC_API void orc_filter2d(const float* src, int H, int W, const float* ker, int kh, int kw,
                           float* dst) {
@@ -99,8 +102,7 @@ ORC_API void orc_filter2d(const float* src, int H, int W, const float* ker, int 
           if (k == 0.0f) continue;
           int xx = x + j - ax;
           float p = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? src[(long)yy * W + xx] : 0.0f;
-          float t = k * p;
-          acc = acc + t;
+          acc = fmaf(k, p, acc);
         }
       }
       dst[(long)y * W + x] = acc;
@@ -483,7 +485,7 @@ ORC_API void orc_descriptors(const float* img, int H, int W, const int64_t* X, c
  * Returns the number of keypoints (or -SFM_E* on error).  level_counts: L ints.
  */
 ORC_API long orc_extract(const float* img, int H, int W, const sfm_params* p, int64_t* X,
-                         int64_t* Y, float* desc, long cap, int32_t* level_counts) {
+                         int64_t* Y, float* desc, float* conf, long cap, int32_t* level_counts) {
   float gk[SFM_MAX_GAUSS * SFM_MAX_GAUSS];
   int gs = p->gaussian_size;
   if (p->gauss_kernel_set) memcpy(gk, p->gauss_kernel, sizeof(float) * gs * gs);
@@ -518,6 +520,7 @@ ORC_API long orc_extract(const float* img, int H, int W, const sfm_params* p, in
     for (long i = 0; i < m; ++i) {
       X[total + i] = (int64_t)((double)xs[i] * scale);   /* (x * scale).astype(int) :101 */
       Y[total + i] = (int64_t)((double)ys[i] * scale);   /* :102 */
+      if (conf) conf[total + i] = cs[i];
     }
     if (level_counts) level_counts[l] = (int32_t)m;
     total += m;

@@ -1,0 +1,236 @@
+"""ctypes binding of libsfmfeat.so (include/sfmfeat.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU is
+visible, the calls raise.  Contexts are per thread (the reference drives extractor and
+matcher from 8 threads, Runner.py:183-191) and per parameter set.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+from . import _abi
+from ._abi import SfmParams
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SFMFEAT_LIB", os.path.join(_HERE, "lib", "libsfmfeat.so"))
+
+_lib = None
+_lib_lock = threading.Lock()
+
+_fp = ctypes.POINTER(ctypes.c_float)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_vp = ctypes.c_void_p
+
+# exported symbol -> (restype, argtypes); every symbol of include/sfmfeat.h
+SIGNATURES = {
+    "sfm_params_default": (None, [ctypes.POINTER(SfmParams), ctypes.c_int32]),
+    "sfm_abi_version": (ctypes.c_int32, []),
+    "sfm_keypoint_capacity": (ctypes.c_int64, [ctypes.POINTER(SfmParams)]),
+    "sfm_pyramid_dims": (ctypes.c_int32, [ctypes.POINTER(SfmParams), ctypes.c_int32, ctypes.c_int32, _i32p]),
+    "sfm_ctx_create": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(SfmParams), ctypes.POINTER(_vp)]),
+    "sfm_ctx_destroy": (ctypes.c_int32, [_vp]),
+    "sfm_last_error": (ctypes.c_char_p, [_vp]),
+    "sfm_extract": (ctypes.c_int32, [_vp, _fp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, _i64p, _i64p,
+                                     _fp, _fp, ctypes.c_int64, _i64p, _i32p]),
+    "sfm_match": (ctypes.c_int32, [_vp, _fp, ctypes.c_int64, _fp, ctypes.c_int64, ctypes.c_float, _i64p, _fp,
+                                   ctypes.c_int64, _i64p]),
+    "sfm_reserve": (ctypes.c_int32, [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "sfm_extract_batch_dev": (ctypes.c_int32, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp, _vp,
+                                               _vp, ctypes.c_int64, _vp]),
+    "sfm_extract_batch_u8_dev": (ctypes.c_int32, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp,
+                                                  _vp, _vp, ctypes.c_int64, _vp]),
+    "sfm_match_pairs_dev": (ctypes.c_int32, [_vp, _vp, _vp, ctypes.c_int32, ctypes.c_int64, _vp, ctypes.c_int32,
+                                             ctypes.c_float, _vp, _vp, _vp, _vp]),
+    "sfm_profile_enable": (ctypes.c_int32, [_vp, ctypes.c_int32]),
+    "sfm_profile_read": (ctypes.c_int32, [_vp, ctypes.POINTER(ctypes.c_double), _i64p, ctypes.c_int32]),
+    "sfm_debug_atan2": (ctypes.c_int32, [ctypes.c_int32, _fp, _fp, _fp, ctypes.c_int64]),
+    "sfm_debug_harris": (ctypes.c_int32, [ctypes.c_int32, _fp, ctypes.c_int32, ctypes.c_double, ctypes.c_int32,
+                                          _fp, ctypes.c_int32, ctypes.c_int32, _fp, _fp, _i64p]),
+}
+
+
+class NativeLibraryMissing(ImportError):
+    pass
+
+
+def load_library(path: str | None = None):
+    """Load libsfmfeat.so and bind every C-ABI symbol (no device call is made)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise NativeLibraryMissing(
+                f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+        L = ctypes.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.sfm_abi_version() != 1:
+            raise NativeLibraryMissing("libsfmfeat ABI version mismatch")
+        if path is None:
+            _lib = L
+        return L
+
+
+def check(rc: int, ctx=None):
+    if rc == _abi.SFM_OK:
+        return
+    msg = ""
+    if ctx is not None and ctx.value:
+        m = load_library().sfm_last_error(ctx)
+        msg = m.decode() if m else ""
+    if rc == _abi.SFM_EINVAL:
+        raise ValueError(msg or "invalid argument")
+    if rc == _abi.SFM_EINDEX:
+        raise IndexError(msg or "index 1 is out of bounds")
+    if rc == _abi.SFM_ESTATE:
+        raise RuntimeError(msg or "call out of order")
+    if rc == _abi.SFM_ERANGE:
+        raise ValueError(msg or "output capacity too small")
+    raise RuntimeError(f"sfmfeat device error: {msg}")
+
+
+def _params_key(p: SfmParams) -> bytes:
+    return bytes(memoryview(p))
+
+
+class Context:
+    """One sfm_ctx (device workspace + HIP stream) for a fixed parameter set."""
+
+    def __init__(self, params: SfmParams, device: int = 0):
+        self.lib = load_library()
+        self.params = params
+        self.device = device
+        h = _vp()
+        rc = self.lib.sfm_ctx_create(device, ctypes.byref(params), ctypes.byref(h))
+        if rc != _abi.SFM_OK:
+            if rc == _abi.SFM_EINVAL:
+                raise ValueError("unsupported extractor parameters for the HIP path")
+            raise RuntimeError("sfm_ctx_create failed: no usable MI355X (HIP) device")
+        self.handle = h
+        self.capacity = int(self.lib.sfm_keypoint_capacity(ctypes.byref(params)))
+        self.levels = 1 if params.mode == _abi.SFM_MODE_NAIVE else int(params.pyramid_level)
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            self.lib.sfm_ctx_destroy(self.handle)
+            self.handle = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -------- host-pointer API (drop-in path) --------
+    def extract(self, img: np.ndarray):
+        """-> X (n,) int64, Y (n,) int64, desc (n,128) float32, conf (n,) float32, level_counts"""
+        if img.dtype != np.float32:
+            img = img.astype(np.float32)
+        if img.strides[1] != 4:
+            img = np.ascontiguousarray(img)
+        H, W = img.shape
+        cap = max(self.capacity, 1)
+        X = np.empty(cap, np.int64)
+        Y = np.empty(cap, np.int64)
+        D = np.empty((cap, 128), np.float32)
+        C = np.empty(cap, np.float32)
+        lc = np.zeros(self.levels, np.int32)
+        n = ctypes.c_int64(0)
+        rc = self.lib.sfm_extract(self.handle, img.ctypes.data_as(_fp), H, W, img.strides[0] // 4,
+                                  X.ctypes.data_as(_i64p), Y.ctypes.data_as(_i64p), D.ctypes.data_as(_fp),
+                                  C.ctypes.data_as(_fp), cap, ctypes.byref(n), lc.ctypes.data_as(_i32p))
+        check(rc, self.handle)
+        k = n.value
+        return X[:k], Y[:k], D[:k], C[:k], lc
+
+    def match(self, d1: np.ndarray, d2: np.ndarray, ratio32: np.float32):
+        d1 = np.ascontiguousarray(d1, dtype=np.float32)
+        d2 = np.ascontiguousarray(d2, dtype=np.float32)
+        n1, n2 = d1.shape[0], d2.shape[0]
+        cap = max(n1, 1)
+        m = np.empty((cap, 2), np.int64)
+        c = np.empty(cap, np.float32)
+        k = ctypes.c_int64(0)
+        rc = self.lib.sfm_match(self.handle, d1.ctypes.data_as(_fp), n1, d2.ctypes.data_as(_fp), n2,
+                                ctypes.c_float(ratio32), m.ctypes.data_as(_i64p), c.ctypes.data_as(_fp), cap,
+                                ctypes.byref(k))
+        check(rc, self.handle)
+        return m[:k.value], c[:k.value]
+
+    # -------- device-pointer API (throughput path; pointers are ints) --------
+    def reserve(self, B: int, H: int, W: int):
+        check(self.lib.sfm_reserve(self.handle, B, H, W), self.handle)
+
+    def extract_batch_dev(self, imgs_ptr: int, B: int, H: int, W: int, xy_ptr: int, desc_ptr: int,
+                          count_ptr: int, cap: int, stream: int = 0, u8: bool = False):
+        fn = self.lib.sfm_extract_batch_u8_dev if u8 else self.lib.sfm_extract_batch_dev
+        check(fn(self.handle, imgs_ptr, B, H, W, xy_ptr, desc_ptr, count_ptr, cap, stream or None), self.handle)
+
+    PROF_STAGES = ["pyramid", "harris", "median", "nms", "topk", "describe", "match_prep", "match",
+                   "match_post"]
+
+    def profile_enable(self, on: bool = True):
+        check(self.lib.sfm_profile_enable(self.handle, 1 if on else 0), self.handle)
+
+    def profile_read(self, reset: bool = True) -> dict:
+        ms = np.zeros(len(self.PROF_STAGES), np.float64)
+        n = np.zeros(len(self.PROF_STAGES), np.int64)
+        check(self.lib.sfm_profile_read(self.handle, ms.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                        n.ctypes.data_as(_i64p), 1 if reset else 0), self.handle)
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.PROF_STAGES)}
+
+    def match_pairs_dev(self, desc_ptr: int, count_ptr: int, nimg: int, cap: int, pairs_ptr: int, P: int,
+                        ratio32: float, matches_ptr: int, conf_ptr: int, nmatch_ptr: int, stream: int = 0):
+        check(self.lib.sfm_match_pairs_dev(self.handle, desc_ptr, count_ptr, nimg, cap, pairs_ptr, P,
+                                           ctypes.c_float(ratio32), matches_ptr, conf_ptr, nmatch_ptr,
+                                           stream or None), self.handle)
+
+
+def debug_atan2(y: np.ndarray, x: np.ndarray, device: int = 0) -> np.ndarray:
+    y = np.ascontiguousarray(y, dtype=np.float32)
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty_like(y)
+    check(load_library().sfm_debug_atan2(device, y.ctypes.data_as(_fp), x.ctypes.data_as(_fp),
+                                         out.ctypes.data_as(_fp), y.size))
+    return out
+
+
+def debug_harris(img: np.ndarray, params: SfmParams, device: int = 0):
+    """-> (R map float32, median float32, candidate count) of one plane."""
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    H, W = img.shape
+    gs = int(params.gaussian_size)
+    g = np.array(params.gauss_kernel[: gs * gs], np.float32)
+    R = np.empty_like(img)
+    med = np.zeros(1, np.float32)
+    nc = ctypes.c_int64(0)
+    check(load_library().sfm_debug_harris(device, g.ctypes.data_as(_fp), gs, params.alpha, params.ksize,
+                                          img.ctypes.data_as(_fp), H, W, R.ctypes.data_as(_fp),
+                                          med.ctypes.data_as(_fp), ctypes.byref(nc)))
+    return R, med[0], nc.value
+
+
+_tls = threading.local()
+
+
+def context_for(params: SfmParams, device: int = 0) -> Context:
+    """Thread-local context cache keyed by (device, parameter bytes)."""
+    cache = getattr(_tls, "cache", None)
+    if cache is None:
+        cache = _tls.cache = {}
+    key = (device, _params_key(params))
+    ctx = cache.get(key)
+    if ctx is None:
+        ctx = cache[key] = Context(params, device)
+    return ctx

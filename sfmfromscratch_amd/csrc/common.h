@@ -1,0 +1,155 @@
+// common.h — device helpers shared by the gfx950 kernels of libsfmfeat.
+//
+// Numeric contract: every kernel is compiled with
+// -ffp-contract=off and correctly rounded f32 division / sqrt, so each arithmetic
+// expression below is one IEEE binary32 (or binary64) operation; fused multiply-adds
+// appear only as explicit __builtin_fmaf where the contract prescribes them.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SFM_DEV __device__ __forceinline__
+
+namespace sfm {
+
+constexpr int kWave = 64;
+
+SFM_DEV uint32_t fbits(float f) { return __float_as_uint(f); }
+SFM_DEV float ffrom(uint32_t u) { return __uint_as_float(u); }
+
+// Order-preserving map float -> uint32 (ascending), -0 folded onto +0 (numpy compares
+// them equal; the median/selection only ever needs the value back).
+SFM_DEV uint32_t fkey(float v) {
+  uint32_t b = __float_as_uint(v);
+  if (b == 0x80000000u) b = 0u;
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+SFM_DEV float fkey_inv(uint32_t k) {
+  uint32_t b = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(b);
+}
+
+// np.arctan2 on float32 as numpy's bundled SVML __svml_atan2f16 computes it
+// (transcription pinned bit-exactly against numpy; oracle/sfm_oracle.c orc_atan2f).
+SFM_DEV float svml_atan2f(float y, float x) {
+  const float PI = __uint_as_float(0x40490fdbu), PI_2 = __uint_as_float(0x3fc90fdbu);
+  float ax = fabsf(x), ay = fabsf(y);
+  uint32_t sy = __float_as_uint(y) & 0x80000000u;
+  uint32_t sx = __float_as_uint(x) & 0x80000000u;
+  if (ay == 0.0f) return __uint_as_float((sx ? __float_as_uint(PI) : 0u) | sy);
+  if (ax == 0.0f) return __uint_as_float(__float_as_uint(PI_2) | sy);
+  bool k = ay < ax;
+  float num = k ? ay : -ax;
+  float den = k ? ax : ay;
+  float off = k ? 0.0f : PI_2;
+  float q = num / den;
+  float z2 = q * q;
+  float z4 = z2 * z2;
+  const float c0 = __uint_as_float(0x3b322cc0u), c1 = __uint_as_float(0xbc7f2631u),
+              c2 = __uint_as_float(0x3d2bc384u), c3 = __uint_as_float(0xbd987629u),
+              c4 = __uint_as_float(0x3dd96474u), c5 = __uint_as_float(0xbe1161f8u),
+              c6 = __uint_as_float(0x3e4cb79fu), c7 = __uint_as_float(0xbeaaaa49u);
+  float A = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(__builtin_fmaf(c0, z4, c2), z4, c4), z4, c6), z4, 1.0f);
+  float B = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(c1, z4, c3), z4, c5), z4, c7);
+  float r = __builtin_fmaf(__builtin_fmaf(B, z2, A), q, off);
+  if (sx) {
+    r = __uint_as_float(__float_as_uint(r) | 0x80000000u);
+    r = r + PI;
+  }
+  return __uint_as_float(__float_as_uint(r) | sy);
+}
+
+// Wave-aggregated append: every lane with `pred` gets a unique slot in [0, *counter).
+// Returns the slot (or -1 for lanes without pred).  One atomic per wave.
+SFM_DEV int64_t wave_append(unsigned long long* counter, bool pred) {
+  uint64_t mask = __ballot(pred);
+  if (mask == 0) return -1;
+  int lane = __lane_id();
+  int leader = __ffsll((unsigned long long)mask) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(mask));
+  base = __shfl(base, leader);
+  uint64_t lower = mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane)));
+  return pred ? (int64_t)(base + __popcll(lower)) : -1;
+}
+
+// Block-wide: given a histogram of `nb` bins in LDS (nb a multiple of blockDim.x), find
+// the bin holding 0-based rank `rank`; s_out = {bin, count before bin}.  s_scan holds
+// blockDim.x uint32.  Every thread of the block must call it.
+SFM_DEV void find_bin(const uint32_t* s_h, int nb, uint32_t rank, uint32_t* s_scan,
+                      uint32_t* s_out) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int per = nb / nt;
+  uint32_t local = 0;
+  for (int i = 0; i < per; ++i) local += s_h[tid * per + i];
+  s_scan[tid] = local;
+  __syncthreads();
+  for (int off = 1; off < nt; off <<= 1) {
+    uint32_t v = (tid >= off) ? s_scan[tid - off] : 0u;
+    __syncthreads();
+    s_scan[tid] += v;
+    __syncthreads();
+  }
+  uint32_t incl = s_scan[tid];
+  uint32_t excl = incl - local;
+  if (rank >= excl && rank < incl) {
+    uint32_t c = excl;
+    for (int i = 0; i < per; ++i) {
+      uint32_t h = s_h[tid * per + i];
+      if (rank < c + h) {
+        s_out[0] = (uint32_t)(tid * per + i);
+        s_out[1] = c;
+        break;
+      }
+      c += h;
+    }
+  }
+  __syncthreads();
+}
+
+// Block-wide exclusive scan of one uint32 per thread; returns the exclusive prefix and
+// writes the block total to *total.  s_scan holds blockDim.x uint32.
+SFM_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_scan, uint32_t* total) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  s_scan[tid] = v;
+  __syncthreads();
+  for (int off = 1; off < nt; off <<= 1) {
+    uint32_t t = (tid >= off) ? s_scan[tid - off] : 0u;
+    __syncthreads();
+    s_scan[tid] += t;
+    __syncthreads();
+  }
+  uint32_t incl = s_scan[tid];
+  *total = s_scan[nt - 1];
+  __syncthreads();
+  return incl - v;
+}
+
+// Block-wide ascending bitonic sort of P (power of two) uint64 keys in LDS.
+SFM_DEV void bitonic_sort_u64(uint64_t* s, int P) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < (P >> 1); i += nt) {
+        int pos = 2 * i - (i & (stride - 1));
+        int partner = pos + stride;
+        bool asc = (pos & size) == 0;
+        uint64_t a = s[pos], b = s[partner];
+        if ((a > b) == asc) {
+          s[pos] = b;
+          s[partner] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+SFM_DEV int next_pow2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+}  // namespace sfm

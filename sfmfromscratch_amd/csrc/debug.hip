@@ -1,0 +1,87 @@
+// debug.hip — diagnostic entry points of the C-ABI (declared in include/sfmfeat.h under
+// "diagnostics").  They expose intermediate stages of the same kernels the pipeline runs
+// so the parity tests can localise a mismatch (device atan2, the Harris R map, the exact
+// median and the candidate count).  Not used by the throughput path.
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/sfmfeat.h"
+#include "kernels.h"
+
+using namespace sfm;
+
+namespace sfm {
+
+__global__ void k_debug_atan2(const float* __restrict__ y, const float* __restrict__ x,
+                              float* __restrict__ out, int64_t n) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = svml_atan2f(y[i], x[i]);
+}
+
+}  // namespace sfm
+
+extern "C" {
+
+int32_t sfm_debug_atan2(int32_t device, const float* y, const float* x, float* out, int64_t n) {
+  if (n <= 0) return SFM_OK;
+  if (hipSetDevice(device) != hipSuccess) return SFM_EDEVICE;
+  float *dy = nullptr, *dx = nullptr, *dout = nullptr;
+  size_t bytes = (size_t)n * 4;
+  if (hipMalloc(&dy, bytes) || hipMalloc(&dx, bytes) || hipMalloc(&dout, bytes)) return SFM_EDEVICE;
+  int32_t rc = SFM_OK;
+  if (hipMemcpy(dy, y, bytes, hipMemcpyHostToDevice) || hipMemcpy(dx, x, bytes, hipMemcpyHostToDevice)) {
+    rc = SFM_EDEVICE;
+  } else {
+    hipLaunchKernelGGL(k_debug_atan2, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dy, dx, dout, n);
+    if (hipDeviceSynchronize() || hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost)) rc = SFM_EDEVICE;
+  }
+  (void)hipFree(dy);
+  (void)hipFree(dx);
+  (void)hipFree(dout);
+  return rc;
+}
+
+// Harris R map, exact median and candidate count of ONE level-0 plane with the
+// context's parameters (NaiveSIFT.py:59-97).
+int32_t sfm_debug_harris(int32_t device, const float* gauss, int32_t gs, double alpha, int32_t ksize,
+                         const float* img, int32_t H, int32_t W, float* R_out, float* median_out,
+                         int64_t* ncand_out) {
+  if (H < 1 || W < 1 || gs < 1 || gs > SFM_MAX_GAUSS) return SFM_EINVAL;
+  if (hipSetDevice(device) != hipSuccess) return SFM_EDEVICE;
+  int64_t n = (int64_t)H * W;
+  float *d_img = nullptr, *d_R = nullptr, *d_g = nullptr;
+  uint32_t *d_hist = nullptr, *d_list = nullptr;
+  MedianState* d_med = nullptr;
+  unsigned long long* d_cnt = nullptr;
+  uint64_t* d_cand = nullptr;
+  int32_t rc = SFM_OK;
+  if (hipMalloc(&d_img, n * 4) || hipMalloc(&d_R, n * 4) || hipMalloc(&d_g, 4 * gs * gs) ||
+      hipMalloc(&d_hist, 4 * kHistBins) || hipMalloc(&d_list, n * 4) || hipMalloc(&d_med, sizeof(MedianState)) ||
+      hipMalloc(&d_cnt, 16) || hipMalloc(&d_cand, n * 8)) {
+    rc = SFM_EDEVICE;
+  } else {
+    hipMemcpy(d_img, img, n * 4, hipMemcpyHostToDevice);
+    hipMemcpy(d_g, gauss, 4 * gs * gs, hipMemcpyHostToDevice);
+    hipMemset(d_hist, 0, 4 * kHistBins);
+    hipMemset(d_cnt, 0, 16);
+    launch_harris(d_img, d_R, d_hist, 1, H, W, d_g, gs, (float)alpha, 0);
+    launch_median(d_R, d_hist, d_med, d_list, d_cnt, 1, H, W, 0);
+    launch_nms(d_R, d_med, d_cand, d_cnt + 1, 1, H, W, ksize, 0);
+    MedianState ms;
+    unsigned long long cnt[2];
+    if (hipDeviceSynchronize() || hipMemcpy(R_out, d_R, n * 4, hipMemcpyDeviceToHost) ||
+        hipMemcpy(&ms, d_med, sizeof(ms), hipMemcpyDeviceToHost) ||
+        hipMemcpy(cnt, d_cnt, 16, hipMemcpyDeviceToHost)) {
+      rc = SFM_EDEVICE;
+    } else {
+      *median_out = ms.median;
+      *ncand_out = (int64_t)cnt[1];
+    }
+  }
+  hipFree(d_img); hipFree(d_R); hipFree(d_g); hipFree(d_hist); hipFree(d_list); hipFree(d_med);
+  hipFree(d_cnt); hipFree(d_cand);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,264 @@
+// describe.hip — 128-D descriptors, one wavefront per keypoint.
+//   rotate = 1: ScaleRotInvSIFT._get_SIFT_descriptors (ScaleRotInvSIFT.py:33-87)
+//   rotate = 0: NaiveSIFT._get_SIFT_descriptors       (NaiveSIFT.py:122-173)
+// Window rows/cols [y-h+1, y+h+1), h = fw // 2 (:53-56).  Gradients are the exact
+// Sobel restatement, magnitude sqrt(Ix^2 + Iy^2), orientation = numpy's SVML atan2f.
+// Every histogram is np.histogram's cumulative path: stable sort of the values, sequential
+// float32 prefix sum of the weights, float64 bin-edge search ('left', last edge 'right'),
+// bin = difference of prefix sums.  RootSIFT: w / ||w|| then sqrt (:82-85), with the
+// fixed-order norm of DESIGN.md §Numerics.
+#include "kernels.h"
+
+namespace sfm {
+
+// numpy.linspace(-pi, pi, num)[i]: i*step + start, last element = stop exactly.
+SFM_DEV double pi_edge(int i, int num) {
+  const double start = -3.141592653589793, stop = 3.141592653589793;
+  if (i == num - 1) return stop;
+  double step = (stop - start) / (double)(num - 1);
+  return (double)i * step + start;
+}
+
+struct DescLayout {
+  int ws, n, pw, P;
+  size_t off_keys, off_cellv, off_patch, off_ori, off_mag, off_cw, off_cellw, off_cellwt, off_wgh,
+      total;
+};
+
+__host__ __device__ inline DescLayout desc_layout(int fw, int rotate) {
+  DescLayout L;
+  int h = fw / 2;
+  L.ws = 2 * h;
+  L.n = L.ws * L.ws;
+  L.pw = L.ws + 2;
+  int P = 1;
+  while (P < L.n) P <<= 1;
+  L.P = P;
+  size_t o = 0;
+  L.off_keys = o;  o += rotate ? (size_t)P * 8 : 0;
+  L.off_cellv = o; o += 16 * 16 * 8;
+  L.off_patch = o; o += (size_t)L.pw * L.pw * 4;
+  L.off_ori = o;   o += (size_t)L.n * 4;
+  L.off_mag = o;   o += (size_t)L.n * 4;
+  L.off_cw = o;    o += rotate ? (size_t)(L.n + 1) * 4 : 0;
+  L.off_cellw = o; o += 16 * 17 * 4;
+  L.off_cellwt = o; o += 16 * 16 * 4;
+  L.off_wgh = o;   o += 128 * 4;
+  o = (o + 15) & ~(size_t)15;
+  L.total = o;
+  return L;
+}
+
+__global__ void __launch_bounds__(64) k_describe(const float* __restrict__ lvl, int H, int W, int fw,
+                                                 int rotate, KpList kp, int kcap,
+                                                 const int32_t* __restrict__ lc_all, int level, int B,
+                                                 double scale, int32_t* __restrict__ out_xy,
+                                                 float* __restrict__ out_desc, float* __restrict__ out_conf,
+                                                 int64_t out_cap) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
+  const int b = blockIdx.y;
+  const int kpi = blockIdx.x;
+  const int count = kp.count[b];
+  if (kpi >= count) return;
+  const int lane = threadIdx.x;
+  const DescLayout Ly = desc_layout(fw, rotate);
+  uint64_t* s_keys = reinterpret_cast<uint64_t*>(s_raw + Ly.off_keys);
+  double* s_cellv = reinterpret_cast<double*>(s_raw + Ly.off_cellv);
+  float* s_patch = reinterpret_cast<float*>(s_raw + Ly.off_patch);
+  float* s_ori = reinterpret_cast<float*>(s_raw + Ly.off_ori);
+  float* s_mag = reinterpret_cast<float*>(s_raw + Ly.off_mag);
+  float* s_cw = reinterpret_cast<float*>(s_raw + Ly.off_cw);
+  float* s_cellw = reinterpret_cast<float*>(s_raw + Ly.off_cellw);
+  float* s_cellwt = reinterpret_cast<float*>(s_raw + Ly.off_cellwt);
+  float* s_wgh = reinterpret_cast<float*>(s_raw + Ly.off_wgh);
+  __shared__ int s_idx[37];
+
+  const int64_t ko = (int64_t)b * kcap + kpi;
+  const int x = kp.x[ko], y = kp.y[ko];
+  const int h = fw / 2, ws = Ly.ws, n = Ly.n, pw = Ly.pw;
+  const float* img = lvl + (int64_t)b * H * W;
+
+  // 1. image patch with one pixel of Sobel halo, zero outside the image
+  for (int e = lane; e < pw * pw; e += 64) {
+    int pr = e / pw, pc = e - pr * pw;
+    int gy = y - h + pr, gx = x - h + pc;
+    float v = 0.0f;
+    if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = img[(int64_t)gy * W + gx];
+    s_patch[e] = v;
+  }
+  __syncthreads();
+  // 2. magnitude / orientation over the 2h x 2h window (ScaleRotInvSIFT.py:40-42)
+  for (int e = lane; e < n; e += 64) {
+    int i = e / ws, j = e - i * ws;
+    const float* c = s_patch + (i + 1) * pw + (j + 1);
+    float a00 = c[-pw - 1], a01 = c[-pw], a02 = c[-pw + 1];
+    float a10 = c[-1], a12 = c[1];
+    float a20 = c[pw - 1], a21 = c[pw], a22 = c[pw + 1];
+    float gx = 0.0f;
+    gx = __builtin_fmaf(-1.0f, a00, gx);
+    gx = __builtin_fmaf(1.0f, a02, gx);
+    gx = __builtin_fmaf(-2.0f, a10, gx);
+    gx = __builtin_fmaf(2.0f, a12, gx);
+    gx = __builtin_fmaf(-1.0f, a20, gx);
+    gx = __builtin_fmaf(1.0f, a22, gx);
+    float gy = 0.0f;
+    gy = __builtin_fmaf(-1.0f, a00, gy);
+    gy = __builtin_fmaf(-2.0f, a01, gy);
+    gy = __builtin_fmaf(-1.0f, a02, gy);
+    gy = __builtin_fmaf(1.0f, a20, gy);
+    gy = __builtin_fmaf(2.0f, a21, gy);
+    gy = __builtin_fmaf(1.0f, a22, gy);
+    float sx = gx * gx;
+    float sy = gy * gy;
+    float s = sx + sy;
+    s_mag[e] = sqrtf(s);
+    s_ori[e] = svml_atan2f(gy, gx);
+  }
+  __syncthreads();
+
+  // 3. dominant orientation (ScaleRotInvSIFT.py:24-31), 36 bins over the whole window
+  double dom = 0.0;
+  if (rotate) {
+    for (int e = lane; e < Ly.P; e += 64)
+      s_keys[e] = (e < n) ? (((uint64_t)fkey(s_ori[e]) << 32) | (uint32_t)e) : ~0ull;
+    __syncthreads();
+    bitonic_sort_u64(s_keys, Ly.P);
+    if (lane == 0) {
+      float acc = 0.0f;
+      s_cw[0] = 0.0f;
+      for (int m = 0; m < n; ++m) {
+        acc = acc + s_mag[(uint32_t)s_keys[m]];
+        s_cw[m + 1] = acc;
+      }
+    }
+    if (lane < 37) {
+      double e = pi_edge(lane, 37);
+      int lo = 0, hi = n;  // first position whose value fails the predicate
+      while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        double v = (double)fkey_inv((uint32_t)(s_keys[mid] >> 32));
+        bool pass = (lane < 36) ? (v < e) : (v <= e);
+        if (pass) lo = mid + 1; else hi = mid;
+      }
+      s_idx[lane] = lo;
+    }
+    __syncthreads();
+    float hb = -INFINITY;
+    int bi = 64;
+    if (lane < 36) {
+      hb = s_cw[s_idx[lane + 1]] - s_cw[s_idx[lane]];
+      bi = lane;
+    }
+    // first argmax: larger value wins, equal values -> smaller bin index
+    for (int off = 32; off >= 1; off >>= 1) {
+      float ov = __shfl_xor(hb, off);
+      int oi = __shfl_xor(bi, off);
+      if (ov > hb || (ov == hb && oi < bi)) { hb = ov; bi = oi; }
+    }
+    dom = (pi_edge(bi, 37) + pi_edge(bi + 1, 37)) / 2.0;
+  }
+
+  // 4. 4 x 4 cells of 4 x 4 px from the window's top-left (:68-76), 8 bins each
+  if (lane < 16) {
+    const int r = lane >> 2, cc = lane & 3;
+    double* cv = s_cellv + lane * 16;
+    float* cw = s_cellw + lane * 17;
+    float* wts = s_cellwt + lane * 16;
+    int cn = 0;
+    for (int i = 4 * r; i < 4 * r + 4 && i < ws; ++i)
+      for (int j = 4 * cc; j < 4 * cc + 4 && j < ws; ++j) {
+        int e = i * ws + j;
+        double ov = (double)s_ori[e];
+        double v = rotate ? ov - dom : ov;   // float64 relative angle (:62)
+        float w = s_mag[e];
+        int p = cn;                           // stable insertion sort by value
+        while (p > 0 && cv[p - 1] > v) {
+          cv[p] = cv[p - 1];
+          wts[p] = wts[p - 1];
+          --p;
+        }
+        cv[p] = v;
+        wts[p] = w;
+        ++cn;
+      }
+    cw[0] = 0.0f;
+    float acc = 0.0f;
+    for (int m = 0; m < cn; ++m) {
+      acc = acc + wts[m];
+      cw[m + 1] = acc;
+    }
+    int idx[9];
+#pragma unroll
+    for (int eb = 0; eb < 9; ++eb) {
+      double e = pi_edge(eb, 9);
+      int c = 0;
+      if (eb < 8) { while (c < cn && cv[c] < e) ++c; }
+      else        { while (c < cn && cv[c] <= e) ++c; }
+      idx[eb] = c;
+    }
+#pragma unroll
+    for (int bb = 0; bb < 8; ++bb) s_wgh[lane * 8 + bb] = cw[idx[bb + 1]] - cw[idx[bb]];
+  }
+  __syncthreads();
+
+  // 5. fixed-order L2 norm, normalise, RootSIFT
+  float w0 = s_wgh[lane], w1 = s_wgh[lane + 64];
+  float a = w0 * w0;
+  float c = w1 * w1;
+  float s = a + c;
+  for (int off = 32; off >= 1; off >>= 1) {
+    float o = __shfl_down(s, off);
+    s = s + o;
+  }
+  float nrm = sqrtf(__shfl(s, 0));
+  int64_t off0 = 0;
+  for (int l = 0; l < level; ++l) off0 += lc_all[(int64_t)l * B + b];
+  const int64_t slot = (int64_t)b * out_cap + off0 + kpi;
+  float v0 = w0, v1 = w1;
+  if (nrm > 0.0f) {
+    v0 = v0 / nrm;
+    v1 = v1 / nrm;
+  }
+  out_desc[slot * 128 + lane] = sqrtf(v0);
+  out_desc[slot * 128 + lane + 64] = sqrtf(v1);
+  if (lane == 0) {
+    if (out_conf) out_conf[slot] = kp.conf[ko];
+    out_xy[slot * 2 + 0] = (int32_t)((double)x * scale);  // (x * scale).astype(int) :101
+    out_xy[slot * 2 + 1] = (int32_t)((double)y * scale);  // :102
+  }
+}
+
+__global__ void k_finalize_counts(const int32_t* __restrict__ lc_all, int B, int L,
+                                  int32_t* __restrict__ out_count) {
+  int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  int32_t s = 0;
+  for (int l = 0; l < L; ++l) s += lc_all[(int64_t)l * B + b];
+  out_count[b] = s;
+}
+
+size_t describe_lds_bytes(int fw, int rotate) { return desc_layout(fw, rotate).total; }
+
+void init_describe_attributes(size_t max_lds) {
+  (void)hipFuncSetAttribute((const void*)k_describe, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)max_lds);
+}
+
+void launch_describe(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp,
+                     int kcap, const int32_t* level_counts_all, int level, int L, double scale,
+                     int32_t* out_xy, float* out_desc, float* out_conf, int64_t out_cap,
+                     hipStream_t st) {
+  (void)L;
+  if (kcap <= 0) return;
+  size_t lds = describe_lds_bytes(fw, rotate);
+  hipLaunchKernelGGL(k_describe, dim3(kcap, B), dim3(64), lds, st, lvl, H, W, fw, rotate, kp, kcap,
+                     level_counts_all, level, B, scale, out_xy, out_desc, out_conf, out_cap);
+}
+
+void launch_finalize_counts(const int32_t* level_counts_all, int B, int L, int32_t* out_count,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(k_finalize_counts, dim3((B + 255) / 256), dim3(256), 0, st, level_counts_all, B, L,
+                     out_count);
+}
+
+}  // namespace sfm

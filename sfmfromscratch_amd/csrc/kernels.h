@@ -1,0 +1,86 @@
+// kernels.h — launcher declarations and the per-plane bookkeeping shared between the
+// host orchestration (sfmfeat.cpp) and the gfx950 kernels.
+//
+// A "plane" is one pyramid level of one image.  All B planes of a level are stored
+// contiguously ([B][h][w]) and are processed by one launch per stage.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace sfm {
+
+#define SFM_NMS_MAX_HALF 15                 // ksize <= 31
+
+constexpr int kHistBits = 12;               // first radix digit of the median select
+constexpr int kHistBins = 1 << kHistBits;   // 4096
+constexpr int kTopkLdsCap = 8192;           // max keys sorted in LDS by the top-k kernel
+constexpr int kMaxMatchRows = 16384;        // max keypoints per image for the matcher sort
+
+// Per-plane state of the exact median (np.median, NaiveSIFT.py:91).
+struct MedianState {
+  uint32_t bucket[2];   // top-12-bit digit holding rank k1 / k2
+  uint32_t rank[2];     // residual rank inside that bucket
+  uint32_t odd;         // H*W odd -> median is element k1 alone
+  float median;         // result
+};
+
+// Per-plane keypoint list produced by the top-k kernel (level coordinates).
+struct KpList {
+  int32_t* x;      // [planes][kcap]
+  int32_t* y;
+  float* conf;
+  int32_t* count;  // [planes]
+};
+
+// pyramid.hip
+void launch_u8_to_f32(const uint8_t* src, float* dst, int64_t n, hipStream_t st);
+void launch_resize(const float* src, int sh, int sw, float* dst, int dh, int dw, int B,
+                   hipStream_t st);
+
+// harris.hip: R map + first median digit histogram (hist zeroed by the caller).
+void launch_harris(const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
+                   const float* d_gauss, int ks, float alpha, hipStream_t st);
+
+// median.hip
+void launch_median(const float* R, uint32_t* hist, MedianState* state, uint32_t* list,
+                   unsigned long long* list_count, int B, int H, int W, hipStream_t st);
+
+// nms.hip: candidates (R == window max, or R == 0 below the median) as 64-bit keys
+// (~fkey(conf) << 32 | raster index), appended per plane.
+void launch_nms(const float* R, const MedianState* state, uint64_t* cand,
+                unsigned long long* cand_count, int B, int H, int W, int ksize, hipStream_t st);
+
+// select.hip: top-k by (conf desc, index asc) + edge filter (NaiveSIFT.py:99-120).
+void init_topk_attributes();
+void init_describe_attributes(size_t max_lds);
+size_t describe_lds_bytes(int fw, int rotate);
+void launch_topk(const uint64_t* cand, const unsigned long long* cand_count, uint64_t* scratch,
+                 KpList kp, int kcap, int k, int B, int H, int W, int half_window,
+                 hipStream_t st);
+
+// describe.hip: descriptors of one level written into the output slot table.
+void launch_describe(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp,
+                     int kcap, const int32_t* level_counts_all, int level, int L, double scale,
+                     int32_t* out_xy, float* out_desc, float* out_conf, int64_t out_cap,
+                     hipStream_t st);
+void launch_finalize_counts(const int32_t* level_counts_all, int B, int L, int32_t* out_count,
+                            hipStream_t st);
+
+// match.hip
+struct RowBest {
+  int32_t col;   // -1: rejected
+  float nndr;
+};
+void launch_transpose_desc(const float* desc, const int32_t* count, int nimg, int64_t cap,
+                           int64_t capP, float* descT, hipStream_t st);
+void launch_match_rows(const float* descT, const int32_t* count, int64_t capP, const int32_t* pairs,
+                       int P, float ratio, RowBest* rows, int max_rows, hipStream_t st);
+void launch_match_compact(const RowBest* rows, const int32_t* count, const int32_t* pairs, int P,
+                          int max_rows, int64_t cap, int32_t* matches, float* conf, int32_t* nmatch,
+                          hipStream_t st);
+void init_match_attributes(int max_rows);
+
+}  // namespace sfm

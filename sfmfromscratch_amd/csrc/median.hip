@@ -1,0 +1,129 @@
+// median.hip — exact np.median of each R plane (NaiveSIFT.py:91), by radix select on
+// order-preserving 32-bit keys of the float32 values.
+//   even H*W: float32 (v[k1] + v[k2]) / 2 with k1 = n/2-1, k2 = n/2
+//   odd  H*W: v[n/2]
+// Digit 1 (top 12 bits) is histogrammed inside the Harris kernel.  Then:
+//   k_med_scan    : one block per plane finds the digit-1 bucket of each rank
+//   k_med_collect : grid pass over R appending the keys that fall in those buckets
+//   k_med_final   : one block per plane resolves digits 2 (12 bits) and 3 (8 bits)
+#include "kernels.h"
+
+namespace sfm {
+
+__global__ void __launch_bounds__(256) k_med_scan(const uint32_t* __restrict__ hist,
+                                                  MedianState* __restrict__ st,
+                                                  unsigned long long* __restrict__ list_count,
+                                                  int64_t n) {
+  __shared__ uint32_t s_h[kHistBins];
+  __shared__ uint32_t s_scan[256];
+  __shared__ uint32_t s_out[2];
+  const int b = blockIdx.x;
+  for (int i = threadIdx.x; i < kHistBins; i += 256) s_h[i] = hist[(int64_t)b * kHistBins + i];
+  __syncthreads();
+  uint32_t k1 = (n % 2 == 1) ? (uint32_t)(n / 2) : (uint32_t)(n / 2 - 1);
+  uint32_t k2 = (uint32_t)(n / 2);
+  find_bin(s_h, kHistBins, k1, s_scan, s_out);
+  uint32_t b1 = s_out[0], r1 = k1 - s_out[1];
+  __syncthreads();
+  find_bin(s_h, kHistBins, k2, s_scan, s_out);
+  uint32_t b2 = s_out[0], r2 = k2 - s_out[1];
+  if (threadIdx.x == 0) {
+    st[b].bucket[0] = b1;
+    st[b].bucket[1] = b2;
+    st[b].rank[0] = r1;
+    st[b].rank[1] = r2;
+    st[b].odd = (uint32_t)(n % 2);
+    list_count[b] = 0ull;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_med_collect(const float* __restrict__ R,
+                                                     const MedianState* __restrict__ st,
+                                                     uint32_t* __restrict__ list,
+                                                     unsigned long long* __restrict__ list_count,
+                                                     int64_t n) {
+  const int b = blockIdx.y;
+  const uint32_t b1 = st[b].bucket[0], b2 = st[b].bucket[1];
+  const float* Rp = R + (int64_t)b * n;
+  uint32_t* lp = list + (int64_t)b * n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - threadIdx.x < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t key = 0;
+    bool pred = false;
+    if (i < n) {
+      key = fkey(Rp[i]);
+      uint32_t d = key >> (32 - kHistBits);
+      pred = (d == b1) || (d == b2);
+    }
+    int64_t slot = wave_append(&list_count[b], pred);
+    if (pred) lp[slot] = key;
+  }
+}
+
+// Resolve one rank within bucket `bk` (the key's top 12 bits) from the collected list.
+SFM_DEV uint32_t select_in_list(const uint32_t* lp, int64_t m, uint32_t bk, uint32_t rank,
+                                uint32_t* s_h, uint32_t* s_scan, uint32_t* s_out) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  // digit 2: bits [19:8]
+  for (int i = tid; i < kHistBins; i += nt) s_h[i] = 0u;
+  __syncthreads();
+  for (int64_t i = tid; i < m; i += nt) {
+    uint32_t k = lp[i];
+    if ((k >> 20) == bk) atomicAdd(&s_h[(k >> 8) & 0xfffu], 1u);
+  }
+  __syncthreads();
+  find_bin(s_h, kHistBins, rank, s_scan, s_out);
+  uint32_t d2 = s_out[0];
+  rank -= s_out[1];
+  uint32_t pre = (bk << 12) | d2;  // top 24 bits
+  __syncthreads();
+  // digit 3: bits [7:0] (histogram padded to 4096 bins for find_bin)
+  for (int i = tid; i < kHistBins; i += nt) s_h[i] = 0u;
+  __syncthreads();
+  for (int64_t i = tid; i < m; i += nt) {
+    uint32_t k = lp[i];
+    if ((k >> 8) == pre) atomicAdd(&s_h[k & 0xffu], 1u);
+  }
+  __syncthreads();
+  find_bin(s_h, kHistBins, rank, s_scan, s_out);
+  uint32_t d3 = s_out[0];
+  __syncthreads();
+  return (pre << 8) | d3;
+}
+
+__global__ void __launch_bounds__(1024) k_med_final(MedianState* __restrict__ st,
+                                                    const uint32_t* __restrict__ list,
+                                                    const unsigned long long* __restrict__ list_count,
+                                                    int64_t n) {
+  __shared__ uint32_t s_h[kHistBins];
+  __shared__ uint32_t s_scan[1024];
+  __shared__ uint32_t s_out[2];
+  const int b = blockIdx.x;
+  const uint32_t* lp = list + (int64_t)b * n;
+  const int64_t m = (int64_t)list_count[b];
+  MedianState s = st[b];
+  uint32_t key1 = select_in_list(lp, m, s.bucket[0], s.rank[0], s_h, s_scan, s_out);
+  float v1 = fkey_inv(key1);
+  float med;
+  if (s.odd) {
+    med = v1;
+  } else {
+    uint32_t key2 = select_in_list(lp, m, s.bucket[1], s.rank[1], s_h, s_scan, s_out);
+    float v2 = fkey_inv(key2);
+    float sum = v1 + v2;
+    med = sum / 2.0f;
+  }
+  if (threadIdx.x == 0) st[b].median = med;
+}
+
+void launch_median(const float* R, uint32_t* hist, MedianState* state, uint32_t* list,
+                   unsigned long long* list_count, int B, int H, int W, hipStream_t st) {
+  int64_t n = (int64_t)H * W;
+  hipLaunchKernelGGL(k_med_scan, dim3(B), dim3(256), 0, st, hist, state, list_count, n);
+  int64_t blocks = (n + 255) / 256;
+  int gx = (int)(blocks < 2048 ? blocks : 2048);
+  hipLaunchKernelGGL(k_med_collect, dim3(gx, B), dim3(256), 0, st, R, state, list, list_count, n);
+  hipLaunchKernelGGL(k_med_final, dim3(B), dim3(1024), 0, st, state, list, list_count, n);
+}
+
+}  // namespace sfm

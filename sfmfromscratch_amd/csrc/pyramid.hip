@@ -1,0 +1,140 @@
+// pyramid.hip — image ingest and the resize pyramid (ScaleRotInvSIFT._build_image_pyramid,
+// ScaleRotInvSIFT.py:109-115: level i = cv2.resize(level i-1, (int(w/s), int(h/s)))).
+//
+// HBM-bound streaming kernels.  Two resize rules (the restatement of cv2.resize
+// INTER_LINEAR on float32):
+//   * exact 2x in both axes -> OpenCV's INTER_AREA-fast switch: ((a00+a01)+(a10+a11))*0.25
+//   * otherwise half-pixel bilinear with OpenCV's coefficient rule.
+// Planes of all B images of one level are contiguous: [B][h][w] float32.
+#include "kernels.h"
+
+namespace sfm {
+
+// uint8 -> float32 value/255 (Runner.py:521).  4 pixels per thread, 16-byte stores.
+__global__ void __launch_bounds__(256) k_u8_to_f32(const uint8_t* __restrict__ src,
+                                                   float* __restrict__ dst, int64_t n) {
+  int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (; i + 3 < n; i += stride) {
+    uchar4 v = *reinterpret_cast<const uchar4*>(src + i);
+    float4 o;
+    o.x = (float)v.x / 255.0f;
+    o.y = (float)v.y / 255.0f;
+    o.z = (float)v.z / 255.0f;
+    o.w = (float)v.w / 255.0f;
+    *reinterpret_cast<float4*>(dst + i) = o;
+  }
+  for (; i < n; ++i) dst[i] = (float)src[i] / 255.0f;
+}
+
+// Exact 2x downscale: each thread produces 2 horizontally adjacent outputs.
+__global__ void __launch_bounds__(256) k_down2(const float* __restrict__ src, int sh, int sw,
+                                               float* __restrict__ dst, int dh, int dw, int B) {
+  int half = (dw + 1) >> 1;
+  int64_t total = (int64_t)B * dh * half;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    int xh = (int)(t % half);
+    int64_t r = t / half;
+    int y = (int)(r % dh);
+    int b = (int)(r / dh);
+    const float* s0 = src + ((int64_t)b * sh + 2 * y) * sw;
+    const float* s1 = s0 + sw;
+    float* d = dst + ((int64_t)b * dh + y) * dw;
+    int x = 2 * xh;
+    {
+      float t0 = s0[2 * x] + s0[2 * x + 1];
+      float t1 = s1[2 * x] + s1[2 * x + 1];
+      d[x] = (t0 + t1) * 0.25f;
+    }
+    if (x + 1 < dw) {
+      float t0 = s0[2 * x + 2] + s0[2 * x + 3];
+      float t1 = s1[2 * x + 2] + s1[2 * x + 3];
+      d[x + 1] = (t0 + t1) * 0.25f;
+    }
+  }
+}
+
+struct LinCoef {
+  int s;
+  float a0, a1;
+  bool single;
+};
+
+// OpenCV INTER_LINEAR coefficient rule (resize.cpp, float path), restated.
+SFM_DEV LinCoef lin_coef(int d, int sn, double scale) {
+  LinCoef c;
+  float f = (float)(((double)d + 0.5) * scale - 0.5);
+  int s = (int)floorf(f);
+  f -= (float)s;
+  c.single = false;
+  if (s < 0) { s = 0; f = 0.0f; }
+  if (s + 1 >= sn) {
+    c.single = true;
+    if (s >= sn - 1) { s = sn - 1; f = 0.0f; }
+  }
+  c.s = s;
+  c.a0 = 1.0f - f;
+  c.a1 = f;
+  return c;
+}
+
+__global__ void __launch_bounds__(256) k_resize_linear(const float* __restrict__ src, int sh, int sw,
+                                                       float* __restrict__ dst, int dh, int dw, int B,
+                                                       double scale_x, double scale_y) {
+  int64_t total = (int64_t)B * dh * dw;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    int x = (int)(t % dw);
+    int64_t r = t / dw;
+    int y = (int)(r % dh);
+    int b = (int)(r / dh);
+    LinCoef cx = lin_coef(x, sw, scale_x);
+    LinCoef cy = lin_coef(y, sh, scale_y);
+    int sy1 = cy.s + 1 < sh ? cy.s + 1 : sh - 1;
+    const float* base = src + (int64_t)b * sh * sw;
+    const float* rows[2] = {base + (int64_t)cy.s * sw, base + (int64_t)sy1 * sw};
+    float h[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const float* S = rows[k];
+      if (cx.single) {
+        h[k] = S[cx.s];
+      } else {
+        float p = S[cx.s] * cx.a0;
+        float q = S[cx.s + 1] * cx.a1;
+        h[k] = p + q;
+      }
+    }
+    float p = h[0] * cy.a0;
+    float q = h[1] * cy.a1;
+    dst[t] = p + q;
+  }
+}
+
+static int grid_for(int64_t n, int per_thread) {
+  int64_t blocks = (n / per_thread + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 8192) blocks = 8192;
+  return (int)blocks;
+}
+
+void launch_u8_to_f32(const uint8_t* src, float* dst, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(k_u8_to_f32, dim3(grid_for(n, 4)), dim3(256), 0, st, src, dst, n);
+}
+
+void launch_resize(const float* src, int sh, int sw, float* dst, int dh, int dw, int B,
+                   hipStream_t st) {
+  if (sh == 2 * dh && sw == 2 * dw) {
+    int64_t n = (int64_t)B * dh * ((dw + 1) / 2);
+    hipLaunchKernelGGL(k_down2, dim3(grid_for(n, 1)), dim3(256), 0, st, src, sh, sw, dst, dh, dw, B);
+  } else {
+    double scale_x = 1.0 / ((double)dw / (double)sw);
+    double scale_y = 1.0 / ((double)dh / (double)sh);
+    int64_t n = (int64_t)B * dh * dw;
+    hipLaunchKernelGGL(k_resize_linear, dim3(grid_for(n, 1)), dim3(256), 0, st, src, sh, sw, dst, dh,
+                       dw, B, scale_x, scale_y);
+  }
+}
+
+}  // namespace sfm

@@ -1,0 +1,564 @@
+// sfmfeat_api.hip — the C-ABI (include/sfmfeat.h): contexts, device workspace and the
+// per-batch launch sequence of the detect + describe + match stage.
+//
+// Launch sequence for a batch of B same-size images (one stream, no host sync inside):
+//   pyramid (L-1 resize launches)
+//   per level: harris(+digit histogram) -> median (scan, collect, final) -> nms/candidates
+//              -> top-k + edge filter
+//   per level: descriptors into the caller's slot table; finalize counts
+// Matching: transpose slot table -> row kernel (exact pairwise distances, best/second)
+//           -> per-pair compaction + (nndr, row) sort.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/sfmfeat.h"
+#include "kernels.h"
+
+using namespace sfm;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct Level {
+  int h, w, fw;
+  double scale;
+};
+
+}  // namespace
+
+struct sfm_ctx {
+  int device = 0;
+  sfm_params p;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int L = 1;
+  int kcap = 0;       // per-level keypoint capacity = int(k / L) (ScaleRotInvSIFT.py:90)
+  int64_t cap = 0;    // per-image capacity = L * kcap
+  float gauss[SFM_MAX_GAUSS * SFM_MAX_GAUSS];
+  DevBuf d_gauss, d_img0, d_lvl, d_R, d_hist, d_med, d_medlist, d_counts, d_cand, d_scratch,
+      d_kpx, d_kpy, d_kpc, d_lc, d_xy, d_desc, d_conf, d_count, d_u8;
+  DevBuf m_desc, m_count, m_pairs, m_descT, m_rows, m_matches, m_conf, m_nmatch;
+  // stage profiling (sfm_profile_*): HIP events bracketing each stage's launches
+  bool prof = false;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
+  std::vector<hipEvent_t> prof_pool;
+  double prof_ms[SFM_PROF_STAGES] = {0};
+  int64_t prof_launches[SFM_PROF_STAGES] = {0};
+};
+
+namespace {
+
+hipEvent_t prof_event(sfm_ctx* c) {
+  if (!c->prof_pool.empty()) {
+    hipEvent_t e = c->prof_pool.back();
+    c->prof_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// RAII bracket: records a start event now and a stop event at scope exit (when enabled).
+struct StageScope {
+  sfm_ctx* c;
+  int stage;
+  hipStream_t st;
+  hipEvent_t a = nullptr, b = nullptr;
+  StageScope(sfm_ctx* c_, int stage_, hipStream_t st_) : c(c_), stage(stage_), st(st_) {
+    if (c->prof) {
+      a = prof_event(c);
+      b = prof_event(c);
+      (void)hipEventRecord(a, st);
+    }
+  }
+  ~StageScope() {
+    if (c->prof) {
+      (void)hipEventRecord(b, st);
+      c->prof_pending.push_back({stage, {a, b}});
+    }
+  }
+};
+
+int set_err(sfm_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                              \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return set_err(ctx, SFM_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+int ensure(sfm_ctx* c, DevBuf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.bytes >= bytes) return SFM_OK;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+  HIPCHK(c, hipMalloc(&b.p, bytes));
+  b.bytes = bytes;
+  return SFM_OK;
+}
+
+template <class T>
+T* as(DevBuf& b) {
+  return reinterpret_cast<T*>(b.p);
+}
+
+void free_buf(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+// NaiveSIFT._generate_gaussian_kernel (NaiveSIFT.py:175-199) evaluated natively in double
+// (numpy's linspace/exp/sum order); the Python wrapper passes numpy's own taps instead.
+void gaussian_taps(int ks, double sigma, float* out) {
+  double ax[SFM_MAX_GAUSS], k[SFM_MAX_GAUSS * SFM_MAX_GAUSS];
+  int m = ks / 2;
+  if (ks == 1) {
+    ax[0] = (double)-m;
+  } else {
+    double step = ((double)m - (double)-m) / (double)(ks - 1);
+    for (int i = 0; i < ks; ++i) ax[i] = (double)i * step + (double)-m;
+    ax[ks - 1] = (double)m;
+  }
+  const double PI = 3.141592653589793;
+  double c = 1.0 / (2.0 * PI * (sigma * sigma));
+  double den = 2.0 * (sigma * sigma);
+  for (int i = 0; i < ks; ++i)
+    for (int j = 0; j < ks; ++j) k[i * ks + j] = c * exp(-((ax[i] * ax[i]) + (ax[j] * ax[j])) / den);
+  int n = ks * ks;
+  double total = 0.0;
+  if (n < 8) {
+    for (int i = 0; i < n; ++i) total += k[i];
+  } else {
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = k[j];
+    int i;
+    for (i = 8; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += k[i + j];
+    total = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) total += k[i];
+  }
+  for (int i = 0; i < n; ++i) out[i] = (float)(k[i] / total);
+}
+
+bool gauss_size_supported(int ks) {
+  return (ks >= 1 && ks <= 9) || ks == 11 || ks == 13 || ks == 15;
+}
+
+int geometry(const sfm_params* p, int H, int W, std::vector<Level>& lv) {
+  int L = p->mode == SFM_MODE_NAIVE ? 1 : p->pyramid_level;
+  if (L < 1 || L > SFM_MAX_LEVELS) return SFM_EINVAL;
+  lv.resize(L);
+  int h = H, w = W;
+  for (int l = 0; l < L; ++l) {
+    if (l > 0) {
+      h = (int)((double)h / p->pyramid_scale_factor);  // int(h / s) (ScaleRotInvSIFT.py:114)
+      w = (int)((double)w / p->pyramid_scale_factor);
+    }
+    if (h <= 0 || w <= 0) return SFM_EINVAL;
+    double scale = p->mode == SFM_MODE_NAIVE ? 1.0 : pow(p->pyramid_scale_factor, (double)l);
+    int fw = p->mode == SFM_MODE_NAIVE ? p->feature_width : (int)((double)p->feature_width / scale);
+    if (p->mode != SFM_MODE_NAIVE && fw < 3) fw = 3;  // min_feature_width (:92,:96)
+    lv[l] = Level{h, w, fw, scale};
+  }
+  return SFM_OK;
+}
+
+int reserve_impl(sfm_ctx* c, int B, int H, int W) {
+  std::vector<Level> lv;
+  if (geometry(&c->p, H, W, lv) != SFM_OK)
+    return set_err(c, SFM_EINVAL, "image too small for the pyramid");
+  int64_t A0 = (int64_t)H * W, Arest = 0;
+  for (int l = 1; l < c->L; ++l) Arest += (int64_t)lv[l].h * lv[l].w;
+  int rc;
+  if ((rc = ensure(c, c->d_img0, (size_t)B * A0 * 4))) return rc;
+  if ((rc = ensure(c, c->d_lvl, (size_t)B * Arest * 4))) return rc;
+  if ((rc = ensure(c, c->d_R, (size_t)B * A0 * 4))) return rc;
+  if ((rc = ensure(c, c->d_hist, (size_t)c->L * B * kHistBins * 4))) return rc;
+  if ((rc = ensure(c, c->d_med, (size_t)c->L * B * sizeof(MedianState)))) return rc;
+  if ((rc = ensure(c, c->d_medlist, (size_t)B * A0 * 4))) return rc;
+  if ((rc = ensure(c, c->d_counts, (size_t)2 * c->L * B * 8))) return rc;
+  if ((rc = ensure(c, c->d_cand, (size_t)B * A0 * 8))) return rc;
+  if ((rc = ensure(c, c->d_scratch, (size_t)B * A0 * 8))) return rc;
+  size_t nk = (size_t)c->L * B * (size_t)std::max(c->kcap, 1);
+  if ((rc = ensure(c, c->d_kpx, nk * 4))) return rc;
+  if ((rc = ensure(c, c->d_kpy, nk * 4))) return rc;
+  if ((rc = ensure(c, c->d_kpc, nk * 4))) return rc;
+  if ((rc = ensure(c, c->d_lc, (size_t)c->L * B * 4))) return rc;
+  return SFM_OK;
+}
+
+int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy, float* desc,
+                 float* conf, int32_t* count, int64_t cap, hipStream_t st) {
+  if (B < 1 || H < 1 || W < 1) return set_err(c, SFM_EINVAL, "empty batch or image");
+  if (cap < c->cap) return set_err(c, SFM_ERANGE, "slot capacity below L * int(k / L)");
+  std::vector<Level> lv;
+  if (geometry(&c->p, H, W, lv) != SFM_OK)
+    return set_err(c, SFM_EINVAL, "image too small for the pyramid");
+  int rc = reserve_impl(c, B, H, W);
+  if (rc) return rc;
+  const int L = c->L;
+  // pyramid
+  std::vector<const float*> lvl(L);
+  lvl[0] = imgs;
+  {
+    StageScope sc(c, SFM_PROF_PYRAMID, st);
+    int64_t off = 0;
+    for (int l = 1; l < L; ++l) {
+      float* dst = as<float>(c->d_lvl) + off;
+      launch_resize(lvl[l - 1], lv[l - 1].h, lv[l - 1].w, dst, lv[l].h, lv[l].w, B, st);
+      lvl[l] = dst;
+      off += (int64_t)B * lv[l].h * lv[l].w;
+    }
+  }
+  HIPCHK(c, hipMemsetAsync(c->d_hist.p, 0, (size_t)L * B * kHistBins * 4, st));
+  HIPCHK(c, hipMemsetAsync(c->d_counts.p, 0, (size_t)2 * L * B * 8, st));
+  unsigned long long* medcnt = as<unsigned long long>(c->d_counts);
+  unsigned long long* candcnt = medcnt + (size_t)L * B;
+  const float alpha = (float)c->p.alpha;  // NEP 50: the python float becomes float32
+  for (int l = 0; l < L; ++l) {
+    const int h = lv[l].h, w = lv[l].w;
+    uint32_t* hist = as<uint32_t>(c->d_hist) + (size_t)l * B * kHistBins;
+    MedianState* med = as<MedianState>(c->d_med) + (size_t)l * B;
+    {
+      StageScope sc(c, SFM_PROF_HARRIS, st);
+      launch_harris(lvl[l], as<float>(c->d_R), hist, B, h, w, as<float>(c->d_gauss), c->p.gaussian_size,
+                    alpha, st);
+    }
+    {
+      StageScope sc(c, SFM_PROF_MEDIAN, st);
+      launch_median(as<float>(c->d_R), hist, med, as<uint32_t>(c->d_medlist), medcnt + (size_t)l * B, B,
+                    h, w, st);
+    }
+    {
+      StageScope sc(c, SFM_PROF_NMS, st);
+      launch_nms(as<float>(c->d_R), med, as<uint64_t>(c->d_cand), candcnt + (size_t)l * B, B, h, w,
+                 c->p.ksize, st);
+    }
+    KpList kp;
+    size_t ko = (size_t)l * B * std::max(c->kcap, 1);
+    kp.x = as<int32_t>(c->d_kpx) + ko;
+    kp.y = as<int32_t>(c->d_kpy) + ko;
+    kp.conf = as<float>(c->d_kpc) + ko;
+    kp.count = as<int32_t>(c->d_lc) + (size_t)l * B;
+    StageScope sc(c, SFM_PROF_TOPK, st);
+    launch_topk(as<uint64_t>(c->d_cand), candcnt + (size_t)l * B, as<uint64_t>(c->d_scratch), kp,
+                std::max(c->kcap, 1), c->kcap, B, h, w, lv[l].fw / 2, st);
+  }
+  const int rotate = c->p.mode == SFM_MODE_NAIVE ? 0 : 1;
+  for (int l = 0; l < L; ++l) {
+    KpList kp;
+    size_t ko = (size_t)l * B * std::max(c->kcap, 1);
+    kp.x = as<int32_t>(c->d_kpx) + ko;
+    kp.y = as<int32_t>(c->d_kpy) + ko;
+    kp.conf = as<float>(c->d_kpc) + ko;
+    kp.count = as<int32_t>(c->d_lc) + (size_t)l * B;
+    StageScope sc(c, SFM_PROF_DESCRIBE, st);
+    launch_describe(lvl[l], B, lv[l].h, lv[l].w, lv[l].fw, rotate, kp, c->kcap, as<int32_t>(c->d_lc), l,
+                    L, lv[l].scale, xy, desc, conf, cap, st);
+  }
+  launch_finalize_counts(as<int32_t>(c->d_lc), B, L, count, st);
+  HIPCHK(c, hipGetLastError());
+  return SFM_OK;
+}
+
+int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, int64_t cap,
+               const int32_t* pairs, int P, float ratio, int32_t* matches, float* conf,
+               int32_t* nmatch, hipStream_t st) {
+  if (P <= 0) return SFM_OK;
+  if (cap < 1 || cap > kMaxMatchRows)
+    return set_err(c, SFM_EINVAL, "match capacity must be in [1, 16384]");
+  int64_t capP = (cap + 63) / 64 * 64;
+  int rc;
+  if ((rc = ensure(c, c->m_descT, (size_t)nimg * 128 * capP * 4))) return rc;
+  if ((rc = ensure(c, c->m_rows, (size_t)P * cap * sizeof(RowBest)))) return rc;
+  {
+    StageScope sc(c, SFM_PROF_MATCH_PREP, st);
+    launch_transpose_desc(desc, count, nimg, cap, capP, as<float>(c->m_descT), st);
+  }
+  {
+    StageScope sc(c, SFM_PROF_MATCH, st);
+    launch_match_rows(as<float>(c->m_descT), count, capP, pairs, P, ratio, as<RowBest>(c->m_rows),
+                      (int)cap, st);
+  }
+  {
+    StageScope sc(c, SFM_PROF_MATCH_POST, st);
+    launch_match_compact(as<RowBest>(c->m_rows), count, pairs, P, (int)cap, cap, matches, conf, nmatch,
+                         st);
+  }
+  HIPCHK(c, hipGetLastError());
+  return SFM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void sfm_params_default(sfm_params* p, int32_t mode) {
+  memset(p, 0, sizeof(*p));
+  p->mode = mode;
+  p->num_interest_points = 2500;  // FeatureExtractor.py:11
+  p->ksize = 7;                   // NaiveSIFT.py:35
+  p->gaussian_size = 7;           // :36
+  p->sigma = 5.0;                 // :37
+  p->alpha = 0.05;                // :38
+  p->feature_width = 16;          // :39
+  p->pyramid_level = mode == SFM_MODE_NAIVE ? 1 : 4;  // ScaleRotInvSIFT.py:12
+  p->pyramid_scale_factor = 2.0;                      // :13
+  p->gauss_kernel_set = 0;
+}
+
+int32_t sfm_abi_version(void) { return 1; }
+
+int64_t sfm_keypoint_capacity(const sfm_params* p) {
+  if (!p) return 0;
+  if (p->mode == SFM_MODE_NAIVE) return p->num_interest_points > 0 ? p->num_interest_points : 0;
+  int L = p->pyramid_level;
+  if (L < 1) return 0;
+  int64_t k = (int64_t)((double)p->num_interest_points / (double)L);
+  return k > 0 ? (int64_t)L * k : 0;
+}
+
+int32_t sfm_pyramid_dims(const sfm_params* p, int32_t H, int32_t W, int32_t* dims) {
+  if (!p || !dims) return SFM_EINVAL;
+  std::vector<Level> lv;
+  if (geometry(p, H, W, lv) != SFM_OK) return SFM_EINVAL;
+  for (size_t l = 0; l < lv.size(); ++l) {
+    dims[2 * l] = lv[l].h;
+    dims[2 * l + 1] = lv[l].w;
+  }
+  return SFM_OK;
+}
+
+int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out) {
+  if (!p || !out) return SFM_EINVAL;
+  *out = nullptr;
+  if (p->mode != SFM_MODE_SCALEROT && p->mode != SFM_MODE_NAIVE) return SFM_EINVAL;
+  if (!gauss_size_supported(p->gaussian_size)) return SFM_EINVAL;
+  if (p->ksize < 0 || p->ksize / 2 > SFM_NMS_MAX_HALF) return SFM_EINVAL;
+  if (p->feature_width < 0 || p->feature_width > SFM_MAX_FW) return SFM_EINVAL;
+  if (p->mode == SFM_MODE_SCALEROT && (p->pyramid_level < 1 || p->pyramid_level > SFM_MAX_LEVELS))
+    return SFM_EINVAL;
+  if (p->mode == SFM_MODE_SCALEROT && !(p->pyramid_scale_factor > 0.0)) return SFM_EINVAL;
+  sfm_ctx* c = new sfm_ctx();
+  c->device = device;
+  c->p = *p;
+  c->L = p->mode == SFM_MODE_NAIVE ? 1 : p->pyramid_level;
+  if (c->p.mode == SFM_MODE_NAIVE) c->p.pyramid_level = 1;
+  int64_t k = p->mode == SFM_MODE_NAIVE ? p->num_interest_points
+                                        : (int64_t)((double)p->num_interest_points / (double)c->L);
+  if (k < 0) k = 0;
+  if (k > kTopkLdsCap || (int64_t)c->L * k > kMaxMatchRows) {
+    delete c;
+    return SFM_EINVAL;
+  }
+  c->kcap = (int)k;
+  c->cap = (int64_t)c->L * k;
+  int gs = p->gaussian_size;
+  if (p->gauss_kernel_set) memcpy(c->gauss, p->gauss_kernel, sizeof(float) * gs * gs);
+  else gaussian_taps(gs, p->sigma, c->gauss);
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return SFM_EDEVICE;
+  }
+  if (ensure(c, c->d_gauss, sizeof(float) * gs * gs) ||
+      hipMemcpy(c->d_gauss.p, c->gauss, sizeof(float) * gs * gs, hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return SFM_EDEVICE;
+  }
+  init_topk_attributes();
+  init_describe_attributes(describe_lds_bytes(SFM_MAX_FW, 1));
+  init_match_attributes(kMaxMatchRows);
+  *out = c;
+  return SFM_OK;
+}
+
+int32_t sfm_ctx_destroy(sfm_ctx* c) {
+  if (!c) return SFM_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  DevBuf* bufs[] = {&c->d_gauss, &c->d_img0, &c->d_lvl, &c->d_R, &c->d_hist, &c->d_med, &c->d_medlist,
+                    &c->d_counts, &c->d_cand, &c->d_scratch, &c->d_kpx, &c->d_kpy, &c->d_kpc, &c->d_lc,
+                    &c->d_xy, &c->d_desc, &c->d_conf, &c->d_count, &c->d_u8, &c->m_desc, &c->m_count, &c->m_pairs,
+                    &c->m_descT, &c->m_rows, &c->m_matches, &c->m_conf, &c->m_nmatch};
+  for (DevBuf* b : bufs) free_buf(*b);
+  for (auto& e : c->prof_pending) {
+    (void)hipEventDestroy(e.second.first);
+    (void)hipEventDestroy(e.second.second);
+  }
+  for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return SFM_OK;
+}
+
+const char* sfm_last_error(const sfm_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int32_t sfm_reserve(sfm_ctx* c, int32_t B, int32_t H, int32_t W) {
+  if (!c || B < 1 || H < 1 || W < 1) return SFM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  return reserve_impl(c, B, H, W);
+}
+
+int32_t sfm_extract_batch_dev(sfm_ctx* c, const float* imgs, int32_t B, int32_t H, int32_t W,
+                              int32_t* xy, float* desc, int32_t* count, int64_t cap, void* stream) {
+  if (!c || !imgs || !xy || !desc || !count) return SFM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  return extract_impl(c, imgs, B, H, W, xy, desc, nullptr, count, cap, st);
+}
+
+int32_t sfm_extract_batch_u8_dev(sfm_ctx* c, const uint8_t* imgs, int32_t B, int32_t H, int32_t W,
+                                 int32_t* xy, float* desc, int32_t* count, int64_t cap, void* stream) {
+  if (!c || !imgs || !xy || !desc || !count || B < 1 || H < 1 || W < 1) return SFM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  int rc = reserve_impl(c, B, H, W);
+  if (rc) return rc;
+  launch_u8_to_f32(imgs, as<float>(c->d_img0), (int64_t)B * H * W, st);
+  return extract_impl(c, as<float>(c->d_img0), B, H, W, xy, desc, nullptr, count, cap, st);
+}
+
+int32_t sfm_extract(sfm_ctx* c, const float* img, int32_t H, int32_t W, int64_t row_stride, int64_t* X,
+                    int64_t* Y, float* desc, float* conf, int64_t cap, int64_t* n_out,
+                    int32_t* level_counts) {
+  if (!c || !img || !n_out) return SFM_EINVAL;
+  if (H < 1 || W < 1 || row_stride < W) return set_err(c, SFM_EINVAL, "bad image shape or stride");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = reserve_impl(c, 1, H, W);
+  if (rc) return rc;
+  const int64_t scap = std::max<int64_t>(c->cap, 1);
+  if ((rc = ensure(c, c->d_xy, (size_t)scap * 8))) return rc;
+  if ((rc = ensure(c, c->d_desc, (size_t)scap * 128 * 4))) return rc;
+  if ((rc = ensure(c, c->d_count, 16))) return rc;
+  if ((rc = ensure(c, c->d_conf, (size_t)scap * 4))) return rc;
+  hipStream_t st = c->stream;
+  HIPCHK(c, hipMemcpy2DAsync(c->d_img0.p, (size_t)W * 4, img, (size_t)row_stride * 4, (size_t)W * 4, H,
+                             hipMemcpyHostToDevice, st));
+  rc = extract_impl(c, as<float>(c->d_img0), 1, H, W, as<int32_t>(c->d_xy), as<float>(c->d_desc),
+                    as<float>(c->d_conf), as<int32_t>(c->d_count), scap, st);
+  if (rc) return rc;
+  int32_t n = 0;
+  std::vector<int32_t> lc(c->L);
+  HIPCHK(c, hipMemcpyAsync(&n, c->d_count.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(lc.data(), c->d_lc.p, (size_t)c->L * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  *n_out = n;
+  if (level_counts) memcpy(level_counts, lc.data(), (size_t)c->L * 4);
+  if (n > cap) return set_err(c, SFM_ERANGE, "output capacity too small");
+  if (n > 0) {
+    std::vector<int32_t> xy((size_t)n * 2);
+    HIPCHK(c, hipMemcpyAsync(xy.data(), c->d_xy.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+    if (desc) HIPCHK(c, hipMemcpyAsync(desc, c->d_desc.p, (size_t)n * 128 * 4, hipMemcpyDeviceToHost, st));
+    if (conf) HIPCHK(c, hipMemcpyAsync(conf, c->d_conf.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    for (int32_t i = 0; i < n; ++i) {
+      if (X) X[i] = xy[2 * i];
+      if (Y) Y[i] = xy[2 * i + 1];
+    }
+  }
+  return SFM_OK;
+}
+
+int32_t sfm_match(sfm_ctx* c, const float* d1, int64_t n1, const float* d2, int64_t n2, float ratio,
+                  int64_t* matches, float* conf, int64_t cap, int64_t* k_out) {
+  if (!c || !k_out || n1 < 0 || n2 < 0) return SFM_EINVAL;
+  if ((n1 > 0 && !d1) || (n2 > 0 && !d2)) return SFM_EINVAL;
+  *k_out = 0;
+  if (n1 >= 1 && n2 < 2) return set_err(c, SFM_EINDEX, "index 1 is out of bounds (fewer than 2 targets)");
+  if (n1 == 0) return SFM_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  int64_t mcap = std::max(n1, n2);
+  if (mcap > kMaxMatchRows) return set_err(c, SFM_EINVAL, "more than 16384 descriptors per side");
+  hipStream_t st = c->stream;
+  int rc;
+  if ((rc = ensure(c, c->m_desc, (size_t)2 * mcap * 128 * 4))) return rc;
+  if ((rc = ensure(c, c->m_count, 16))) return rc;
+  if ((rc = ensure(c, c->m_pairs, 16))) return rc;
+  if ((rc = ensure(c, c->m_matches, (size_t)mcap * 8))) return rc;
+  if ((rc = ensure(c, c->m_conf, (size_t)mcap * 4))) return rc;
+  if ((rc = ensure(c, c->m_nmatch, 16))) return rc;
+  int32_t hcount[2] = {(int32_t)n1, (int32_t)n2};
+  int32_t hpairs[2] = {0, 1};
+  float* dd = as<float>(c->m_desc);
+  HIPCHK(c, hipMemcpyAsync(dd, d1, (size_t)n1 * 128 * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(dd + mcap * 128, d2, (size_t)n2 * 128 * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->m_count.p, hcount, 8, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->m_pairs.p, hpairs, 8, hipMemcpyHostToDevice, st));
+  rc = match_impl(c, dd, as<int32_t>(c->m_count), 2, mcap, as<int32_t>(c->m_pairs), 1, ratio,
+                  as<int32_t>(c->m_matches), as<float>(c->m_conf), as<int32_t>(c->m_nmatch), st);
+  if (rc) return rc;
+  int32_t k = 0;
+  HIPCHK(c, hipMemcpyAsync(&k, c->m_nmatch.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  if (k < 0) return set_err(c, SFM_EINDEX, "index 1 is out of bounds (fewer than 2 targets)");
+  *k_out = k;
+  if (k > cap) return set_err(c, SFM_ERANGE, "output capacity too small");
+  if (k > 0) {
+    std::vector<int32_t> mm((size_t)k * 2);
+    HIPCHK(c, hipMemcpyAsync(mm.data(), c->m_matches.p, (size_t)k * 8, hipMemcpyDeviceToHost, st));
+    if (conf) HIPCHK(c, hipMemcpyAsync(conf, c->m_conf.p, (size_t)k * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    if (matches)
+      for (int64_t i = 0; i < 2 * k; ++i) matches[i] = mm[i];
+  }
+  return SFM_OK;
+}
+
+int32_t sfm_profile_enable(sfm_ctx* c, int32_t on) {
+  if (!c) return SFM_EINVAL;
+  c->prof = on != 0;
+  return SFM_OK;
+}
+
+int32_t sfm_profile_read(sfm_ctx* c, double* ms, int64_t* launches, int32_t reset) {
+  if (!c) return SFM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  for (auto& e : c->prof_pending) {
+    HIPCHK(c, hipEventSynchronize(e.second.second));
+    float t = 0.0f;
+    HIPCHK(c, hipEventElapsedTime(&t, e.second.first, e.second.second));
+    c->prof_ms[e.first] += t;
+    c->prof_launches[e.first] += 1;
+    c->prof_pool.push_back(e.second.first);
+    c->prof_pool.push_back(e.second.second);
+  }
+  c->prof_pending.clear();
+  for (int i = 0; i < SFM_PROF_STAGES; ++i) {
+    if (ms) ms[i] = c->prof_ms[i];
+    if (launches) launches[i] = c->prof_launches[i];
+    if (reset) {
+      c->prof_ms[i] = 0.0;
+      c->prof_launches[i] = 0;
+    }
+  }
+  return SFM_OK;
+}
+
+int32_t sfm_match_pairs_dev(sfm_ctx* c, const float* desc, const int32_t* count, int32_t nimg,
+                            int64_t cap, const int32_t* pairs, int32_t P, float ratio, int32_t* matches,
+                            float* conf, int32_t* nmatch, void* stream) {
+  if (!c || !desc || !count || !pairs || !matches || !conf || !nmatch || nimg < 1 || P < 0)
+    return SFM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  return match_impl(c, desc, count, nimg, cap, pairs, P, ratio, matches, conf, nmatch, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,96 @@
+"""Device-resident batch API over the C-ABI (the throughput path).
+
+torch is used only as device-memory / stream plumbing: tensors hand their data pointers
+to libsfmfeat, and the library enqueues on torch's current HIP stream so its kernels are
+ordered with any torch work around them.
+
+Slot table: xy [B, cap, 2] int32, desc [B, cap, 128] float32,
+count [B] int32, cap = L * int(k / L).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _abi
+from ._native import Context
+from .matcher import ratio_as_float32
+
+
+def consecutive_pairs(n: int, offset: int = 0) -> np.ndarray:
+    """(i, i+1) pairs of the reference's schedule (Runner.py:183)."""
+    i = np.arange(max(n - 1, 0), dtype=np.int32) + offset
+    return np.stack([i, i + 1], axis=1).astype(np.int32)
+
+
+def all_pairs(n: int) -> np.ndarray:
+    i, j = np.triu_indices(n, k=1)
+    return np.stack([i, j], axis=1).astype(np.int32)
+
+
+class SlotTable:
+    def __init__(self, torch, B: int, cap: int, device):
+        self.B, self.cap = B, cap
+        self.xy = torch.zeros((B, max(cap, 1), 2), dtype=torch.int32, device=device)
+        self.desc = torch.zeros((B, max(cap, 1), 128), dtype=torch.float32, device=device)
+        self.count = torch.zeros((B,), dtype=torch.int32, device=device)
+
+
+class BatchExtractor:
+    """Batched ScaleRotInvSIFT / NaiveSIFT extraction on device-resident frames."""
+
+    def __init__(self, extractor_params: dict | None = None, mode: str = "scalerot", device: int = 0):
+        import torch
+        self.torch = torch
+        self.mode = _abi.SFM_MODE_NAIVE if mode == "naive" else _abi.SFM_MODE_SCALEROT
+        self.params = _abi.params_from_dict(extractor_params, self.mode)
+        self.device = device
+        self.ctx = Context(self.params, device)
+        self.cap = self.ctx.capacity
+
+    def reserve(self, B: int, H: int, W: int):
+        self.ctx.reserve(B, H, W)
+
+    def new_slots(self, B: int) -> SlotTable:
+        return SlotTable(self.torch, B, self.cap, f"cuda:{self.device}")
+
+    def extract(self, imgs, out: SlotTable | None = None) -> SlotTable:
+        torch = self.torch
+        assert imgs.is_cuda and imgs.dim() == 3 and imgs.is_contiguous()
+        B, H, W = imgs.shape
+        if out is None:
+            out = self.new_slots(B)
+        stream = torch.cuda.current_stream(imgs.device).cuda_stream
+        self.ctx.extract_batch_dev(imgs.data_ptr(), B, H, W, out.xy.data_ptr(), out.desc.data_ptr(),
+                                   out.count.data_ptr(), max(self.cap, 1), stream,
+                                   u8=(imgs.dtype == torch.uint8))
+        return out
+
+
+class BatchMatcher:
+    """NNRatioFeatureMatcher over image pairs of a slot table."""
+
+    def __init__(self, ratio_threshold=0.8, device: int = 0, ctx: Context | None = None):
+        import torch
+        self.torch = torch
+        self.ratio32 = float(ratio_as_float32(ratio_threshold))
+        self.ctx = ctx or Context(_abi.params_from_dict({}, _abi.SFM_MODE_NAIVE), device)
+        self.device = device
+
+    def match(self, slots: SlotTable, pairs, out=None):
+        """pairs: (P, 2) int32 tensor on the device.  Returns (matches [P,cap,2] int32,
+        conf [P,cap] f32, nmatch [P] int32 (-1 = the reference's IndexError))."""
+        torch = self.torch
+        P = int(pairs.shape[0])
+        cap = slots.desc.shape[1]
+        dev = slots.desc.device
+        if out is None:
+            out = (torch.zeros((max(P, 1), cap, 2), dtype=torch.int32, device=dev),
+                   torch.zeros((max(P, 1), cap), dtype=torch.float32, device=dev),
+                   torch.zeros((max(P, 1),), dtype=torch.int32, device=dev))
+        if P == 0:
+            return out
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        self.ctx.match_pairs_dev(slots.desc.data_ptr(), slots.count.data_ptr(), slots.desc.shape[0], cap,
+                                 pairs.data_ptr(), P, self.ratio32, out[0].data_ptr(), out[1].data_ptr(),
+                                 out[2].data_ptr(), stream)
+        return out

@@ -61,6 +61,30 @@ def assert_keypoints_equal(x_ref, y_ref, x, y, c_ref=None, c=None):
         i = j
 
 
+def tie_permutation(x_ref, y_ref, x, y, conf):
+    """Permutation `perm` with x[perm] == x_ref, y[perm] == y_ref, allowed to reorder only
+    inside runs of equal confidence (the reference orders ties with an unstable argsort).
+    Asserts that such a permutation exists."""
+    x_ref, y_ref, x, y = (np.asarray(a) for a in (x_ref, y_ref, x, y))
+    conf = np.asarray(conf, np.float32)
+    assert len(x_ref) == len(x), (len(x_ref), len(x))
+    perm = np.arange(len(x))
+    i, n = 0, len(x)
+    while i < n:
+        j = i + 1
+        while j < n and conf[j] == conf[i]:
+            j += 1
+        if j - i > 1 or x[i] != x_ref[i] or y[i] != y_ref[i]:
+            ours = {(int(x[t]), int(y[t])): t for t in range(i, j)}
+            for t in range(i, j):
+                key = (int(x_ref[t]), int(y_ref[t]))
+                assert key in ours, f"keypoint {t} {key} not in tie group {i}:{j}"
+                perm[t] = ours[key]
+        i = j
+    assert np.array_equal(x[perm], x_ref) and np.array_equal(y[perm], y_ref)
+    return perm
+
+
 def assert_matches_equal(m_ref, c_ref, m, c):
     """Matches identical; runs of equal nndr compared as sets (argsort unstable)."""
     m_ref = np.asarray(m_ref).reshape(-1, 2)

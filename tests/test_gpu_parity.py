@@ -1,0 +1,250 @@
+"""GPU parity: the HIP path (through the C-ABI) against the golden fixtures generated from
+the reference and against the C oracle on the same seeded inputs.
+
+Bars: keypoint X/Y and match pairs bit-identical (ties as sets);
+descriptors within 1e-4 relative of the reference (tests/golden_util.desc_close) and
+BIT-identical to the oracle, which shares the restated norm order.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from sfmfromscratch_amd import NaiveSIFT, NNRatioFeatureMatcher, ScaleRotInvSIFT, _abi, _native, synth
+from tests.golden_util import (P_MAIN, P_OCT, assert_keypoints_equal, assert_matches_equal, desc_close, frame,
+                               load, params_of, tie_permutation)
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def test_device_atan2_bitexact():
+    z = load("atan2.npz")
+    out = _native.debug_atan2(z["y"], z["x"])
+    assert np.array_equal(bits(out), bits(z["out"]))
+
+
+@pytest.mark.parametrize("H,W,pp", [(120, 160, P_MAIN), (97, 131, P_MAIN), (120, 160, {}),
+                                    (64, 64, dict(P_MAIN, gaussian_size=5, sigma=2.5)),
+                                    (33, 70, dict(P_MAIN, gaussian_size=3, ksize=5))])
+def test_harris_R_median_bitexact_vs_oracle(H, W, pp):
+    img = synth.make_frame(H, W, 17, 1)
+    p = _abi.params_from_dict(pp, _abi.SFM_MODE_SCALEROT)
+    R, med, ncand = _native.debug_harris(img, p)
+    Ro = O.harris_response(img, pp)
+    assert np.array_equal(bits(R), bits(Ro))
+    assert np.float32(med) == O.median(Ro)
+    _, _, _, dbg = O.detect(img, 10 ** 7, 0, pp, debug=True)
+    assert ncand == dbg["n_candidates"]
+
+
+DETECT_CASES = [
+    (120, 160, 7, 0, 300, 18, P_MAIN),
+    (120, 160, 7, 0, 300, 16, {}),
+    (97, 131, 3, 2, 200, 9, P_MAIN),
+    (96, 128, 4, 0, 1000, 4, dict(P_MAIN, ksize=5, alpha=0.04)),
+    (64, 64, 5, 0, 50, 3, dict(P_MAIN, gaussian_size=5, sigma=2.5)),
+    (30, 41, 6, 0, 100, 18, P_MAIN),
+]
+
+
+@pytest.mark.parametrize("i", range(len(DETECT_CASES)))
+def test_naive_detect_vs_golden(i):
+    z = load("detect.npz")
+    H, W, seed, idx, k, fw, pp = DETECT_CASES[i]
+    img = frame(H, W, seed, idx, z[f"c{i}_sha"])
+    ns = NaiveSIFT(img, dict(pp, num_interest_points=k, feature_width=fw))
+    x, y = ns.detect_keypoints()
+    assert x.dtype == np.int64 and y.dtype == np.int64
+    assert_keypoints_equal(z[f"c{i}_x"], z[f"c{i}_y"], x, y, z[f"c{i}_c"], ns.confidences)
+
+
+def test_descriptors_vs_golden_all_widths():
+    z = load("descriptors.npz")
+    for i in range(int(z["ncases"])):
+        H, W, seed, idx, fw, rotate = (int(v) for v in z[f"c{i}_meta"])
+        img = frame(H, W, seed, idx, z[f"c{i}_sha"])
+        pp = dict(P_MAIN, num_interest_points=120, feature_width=fw)
+        if rotate:
+            obj = ScaleRotInvSIFT(img, dict(pp, pyramid_level=1))
+            x, y = obj.detect_keypoints()
+            d = obj.extract_descriptors()
+        else:
+            obj = NaiveSIFT(img, pp)
+            x, y = obj.detect_keypoints()
+            d = obj.extract_descriptors()
+        assert np.array_equal(x, z[f"c{i}_x"]) and np.array_equal(y, z[f"c{i}_y"]), (fw, rotate)
+        assert desc_close(z[f"c{i}_d"], d), (fw, rotate)
+        od = O.descriptors(img, x, y, fw, bool(rotate))
+        assert np.array_equal(bits(d), bits(od)), (fw, rotate)
+
+
+EXTRACT_FIXTURES = ["extract_small_scalerot.npz", "extract_small_pmain.npz", "extract_small_naive.npz",
+                    "extract_small_defaults.npz", "extract_c1_640x480_pmain.npz", "extract_c2_1080p_poct.npz"]
+
+
+@pytest.mark.parametrize("name", EXTRACT_FIXTURES)
+def test_extract_and_match_vs_golden_and_oracle(name):
+    z = load(name)
+    H, W, seed, nframes, stride = (int(v) for v in z["meta"])
+    pp = params_of(z)
+    naive = str(z["mode"]) == "naive"
+    descs = []
+    for f in range(nframes):
+        img = frame(H, W, seed, f, z[f"f{f}_sha"])
+        if naive:
+            obj = NaiveSIFT(img, pp)
+            X, Y = obj.detect_keypoints()
+            D = obj.extract_descriptors()
+        else:
+            obj = ScaleRotInvSIFT(img, pp)
+            X, Y = obj.detect_keypoints()
+            D = obj.extract_descriptors()
+        assert D.dtype == np.float32 and D.shape == (len(X), 128)
+        perm = tie_permutation(z[f"f{f}_X"], z[f"f{f}_Y"], X, Y, obj.confidences)
+        assert desc_close(z[f"f{f}_D"], D[perm][::stride])
+        OX, OY, OD, _, OC = O.extract(img, pp, mode=1 if naive else 0, with_conf=True)
+        assert np.array_equal(X, OX) and np.array_equal(Y, OY)
+        assert np.array_equal(bits(obj.confidences), bits(OC))
+        assert np.array_equal(bits(D), bits(OD))
+        descs.append(D)
+    if "matches" in z.files:
+        ratio = float(z["ratio"])
+        m, c = NNRatioFeatureMatcher(ratio).match_features_ratio_test(descs[0], descs[1])
+        om, oc = O.match(descs[0], descs[1], ratio)
+        assert_matches_equal(om, oc, m, c)
+        a = set(map(tuple, z["matches"].tolist()))
+        b = set(map(tuple, m.tolist()))
+        assert len(a ^ b) <= max(1, 0.01 * len(a)), (len(a), len(b))
+
+
+def test_matcher_vs_golden_tables():
+    z = load("match.npz")
+    for i in range(int(z["ncases"])):
+        n1, s1, n2, s2, jit = (int(v) for v in z[f"c{i}_meta"])
+        a, ha = synth.make_descriptor_table(n1, s1)
+        b, _ = synth.make_descriptor_table(n2, s2, dup_of=ha, jitter=jit)
+        m, c = NNRatioFeatureMatcher(float(z[f"c{i}_ratio"])).match_features_ratio_test(a, b)
+        if len(z[f"c{i}_c"]) == 0:
+            assert m.shape == (0,)
+        else:
+            assert_matches_equal(z[f"c{i}_m"], z[f"c{i}_c"], m, c)
+
+
+@pytest.mark.parametrize("n1,n2,ratio", [(1, 2, 0.8), (5, 700, 0.9), (333, 65, 0.7), (2500, 2400, 0.85),
+                                         (64, 64, 1.0)])
+def test_matcher_vs_oracle_sizes(n1, n2, ratio):
+    a, ha = synth.make_descriptor_table(n1, 100 + n1)
+    b, _ = synth.make_descriptor_table(n2, 200 + n2, dup_of=ha, jitter=2)
+    m, c = NNRatioFeatureMatcher(ratio).match_features_ratio_test(a, b)
+    om, oc = O.match(a, b, ratio)
+    if len(oc) == 0:
+        assert m.shape == (0,)
+    else:
+        assert_matches_equal(om, oc, m, c)
+
+
+def test_matcher_index_error_and_empty():
+    a, _ = synth.make_descriptor_table(4, 1)
+    with pytest.raises(IndexError):
+        NNRatioFeatureMatcher().match_features_ratio_test(a, a[:1])
+    # identical sets: every nearest distance is 0 with a non-zero second -> nndr 0
+    m, c = NNRatioFeatureMatcher(0.5).match_features_ratio_test(a, a)
+    assert np.array_equal(np.sort(m[:, 0]), np.arange(4)) and np.all(c == 0)
+
+
+def test_ragged_single_keypoint_level_mirrors_reference():
+    # a level that yields exactly one keypoint is extended element-wise by the reference
+    # (ScaleRotInvSIFT.py:103); numpy 2 then refuses the inhomogeneous list
+    img = synth.make_frame(64, 64, 3, 0)
+    pp = dict(P_OCT, num_interest_points=8, pyramid_level=2)
+    X, Y, D, lc = O.extract(img, pp)
+    if 1 in lc.tolist() and lc.sum() > 1:
+        with pytest.raises(ValueError):
+            ScaleRotInvSIFT(img, pp)
+    else:
+        obj = ScaleRotInvSIFT(img, pp)
+        assert np.array_equal(obj.detect_keypoints()[0], X)
+
+
+def test_empty_outputs_like_reference():
+    img = np.full((40, 40), 0.5, np.float32)  # flat: only R == 0 candidates
+    obj = ScaleRotInvSIFT(img, dict(P_OCT, num_interest_points=0))
+    X, Y = obj.detect_keypoints()
+    assert X.shape == (0,) and X.dtype == np.float64
+    assert obj.extract_descriptors().shape == (0,)
+
+
+def test_flat_image_ties_match_oracle():
+    img = np.full((48, 50), 0.25, np.float32)
+    pp = dict(P_MAIN, num_interest_points=40, feature_width=4)
+    ns = NaiveSIFT(img, pp)
+    x, y = ns.detect_keypoints()
+    ox, oy, oc = O.detect(img, 40, 4, pp)
+    assert np.array_equal(x, ox) and np.array_equal(y, oy)
+
+
+def test_batch_api_u8_and_f32_agree_with_oracle():
+    torch = pytest.importorskip("torch")
+    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, consecutive_pairs
+    B, H, W = 4, 135, 240
+    u8 = synth.make_batch_u8(B, H, W, seed=77)
+    pp = dict(P_OCT, num_interest_points=400)
+    ex = BatchExtractor(pp)
+    t_u8 = torch.from_numpy(u8).cuda()
+    t_f32 = torch.from_numpy(synth.u8_to_gray(u8)).cuda()
+    s1 = ex.extract(t_u8)
+    s2 = ex.extract(t_f32)
+    torch.cuda.synchronize()
+    for k in ("xy", "desc", "count"):
+        assert torch.equal(getattr(s1, k), getattr(s2, k))
+    pairs = torch.from_numpy(consecutive_pairs(B)).cuda()
+    mm, mc, nm = BatchMatcher(0.85).match(s1, pairs)
+    torch.cuda.synchronize()
+    counts = s1.count.cpu().numpy()
+    xy = s1.xy.cpu().numpy()
+    desc = s1.desc.cpu().numpy()
+    for b in range(B):
+        X, Y, D, _ = O.extract(synth.u8_to_gray(u8[b]), pp)
+        n = counts[b]
+        assert n == len(X)
+        assert np.array_equal(xy[b, :n, 0], X) and np.array_equal(xy[b, :n, 1], Y)
+        assert np.array_equal(bits(desc[b, :n]), bits(D))
+    for p in range(B - 1):
+        i, j = p, p + 1
+        om, oc = O.match(desc[i, :counts[i]], desc[j, :counts[j]], 0.85)
+        k = int(nm[p])
+        assert_matches_equal(om, oc, mm[p, :k].cpu().numpy(), mc[p, :k].cpu().numpy())
+
+
+def test_1080p_batch_consistency_and_golden():
+    """Full BASELINE size: every copy of the golden 1080p frames in one batch gives the
+    golden keypoints (batch independence + parity at the metric's configuration)."""
+    torch = pytest.importorskip("torch")
+    from sfmfromscratch_amd.pipeline import BatchExtractor
+    z = load("extract_c2_1080p_poct.npz")
+    H, W, seed = (int(v) for v in z["meta"][:3])
+    pp = params_of(z)
+    frames = np.stack([synth.make_frame_u8(H, W, seed, f % 2) for f in range(6)])
+    ex = BatchExtractor(pp)
+    s = ex.extract(torch.from_numpy(frames).cuda())
+    torch.cuda.synchronize()
+    counts = s.count.cpu().numpy()
+    xy = s.xy.cpu().numpy()
+    desc = s.desc.cpu().numpy()
+    for b in range(6):
+        f = b % 2
+        n = counts[b]
+        if b < 2:
+            OX, OY, OD, _, OC = O.extract(synth.u8_to_gray(frames[b]), pp, with_conf=True)
+            assert n == len(OX)
+            assert np.array_equal(xy[b, :n, 0], OX) and np.array_equal(xy[b, :n, 1], OY)
+            assert np.array_equal(bits(desc[b, :n]), bits(OD))
+            perm = tie_permutation(z[f"f{f}_X"], z[f"f{f}_Y"], OX, OY, OC)
+            assert desc_close(z[f"f{f}_D"], desc[b, :n][perm][::8])
+        assert np.array_equal(xy[b, :n], xy[f, :n])
+        assert np.array_equal(bits(desc[b, :n]), bits(desc[f, :n]))
