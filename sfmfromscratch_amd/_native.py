@@ -59,12 +59,34 @@ class NativeLibraryMissing(ImportError):
     pass
 
 
+def _preload_torch_hip_runtime():
+    """If PyTorch-ROCm is installed, load ITS libamdhip64 first (without importing torch).
+
+    torch bundles its own HIP runtime with the same SONAME as /opt/rocm's; whichever is
+    loaded first serves the whole process.  Loading torch's copy up front keeps one
+    runtime for both libsfmfeat and torch whatever the import order (device pointers and
+    streams are then shared); without torch the system runtime is used."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        cand = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(cand):
+            try:
+                ctypes.CDLL(cand, mode=ctypes.RTLD_GLOBAL)
+            except OSError:
+                pass
+            return
+
+
 def load_library(path: str | None = None):
     """Load libsfmfeat.so and bind every C-ABI symbol (no device call is made)."""
     global _lib
     with _lib_lock:
         if _lib is not None and path is None:
             return _lib
+        _preload_torch_hip_runtime()
         p = path or LIB_PATH
         if not os.path.exists(p):
             raise NativeLibraryMissing(

@@ -74,6 +74,36 @@ SFM_DEV int64_t wave_append(unsigned long long* counter, bool pred) {
   return pred ? (int64_t)(base + __popcll(lower)) : -1;
 }
 
+// Block-wide append with ONE global atomic per workgroup (same-address atomics serialise
+// at ~88/us on MI355X, MI355X_MICROARCH.md 'dequeue'): every thread contributes `cnt`
+// items; returns the thread's first slot.  Item order inside the block is thread order.
+// s_wsum: >= blockDim.x/64 uint32; s_base: one uint64.  Every thread must call it.
+SFM_DEV int64_t block_append(unsigned long long* counter, uint32_t cnt, uint32_t* s_wsum,
+                             unsigned long long* s_base) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+  uint32_t x = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    uint32_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_wsum[wid] = x;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t run = 0;
+    for (int w = 0; w < nw; ++w) {
+      uint32_t t = s_wsum[w];
+      s_wsum[w] = run;
+      run += t;
+    }
+    *s_base = run ? atomicAdd(counter, (unsigned long long)run) : 0ull;
+  }
+  __syncthreads();
+  int64_t r = (int64_t)(*s_base + s_wsum[wid] + (x - cnt));
+  __syncthreads();
+  return r;
+}
+
 // Block-wide: given a histogram of `nb` bins in LDS (nb a multiple of blockDim.x), find
 // the bin holding 0-based rank `rank`; s_out = {bin, count before bin}.  s_scan holds
 // blockDim.x uint32.  Every thread of the block must call it.

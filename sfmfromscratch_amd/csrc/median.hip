@@ -37,27 +37,39 @@ __global__ void __launch_bounds__(256) k_med_scan(const uint32_t* __restrict__ h
   }
 }
 
+constexpr int kCollectPerThread = 16;
+
+// Each workgroup scans 256 * 16 consecutive keys and appends the ones in the two target
+// buckets with one global atomic (block_append).
 __global__ void __launch_bounds__(256) k_med_collect(const float* __restrict__ R,
                                                      const MedianState* __restrict__ st,
                                                      uint32_t* __restrict__ list,
                                                      unsigned long long* __restrict__ list_count,
                                                      int64_t n) {
+  __shared__ uint32_t s_wsum[4];
+  __shared__ unsigned long long s_base;
   const int b = blockIdx.y;
   const uint32_t b1 = st[b].bucket[0], b2 = st[b].bucket[1];
   const float* Rp = R + (int64_t)b * n;
-  uint32_t* lp = list + (int64_t)b * n;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - threadIdx.x < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    uint32_t key = 0;
-    bool pred = false;
+  const int64_t base = (int64_t)blockIdx.x * 256 * kCollectPerThread;
+  uint32_t keys[kCollectPerThread];
+  uint32_t mask = 0;
+#pragma unroll
+  for (int q = 0; q < kCollectPerThread; ++q) {
+    int64_t i = base + (int64_t)q * 256 + threadIdx.x;  // coalesced
+    keys[q] = 0;
     if (i < n) {
-      key = fkey(Rp[i]);
+      uint32_t key = fkey(Rp[i]);
       uint32_t d = key >> (32 - kHistBits);
-      pred = (d == b1) || (d == b2);
+      keys[q] = key;
+      if (d == b1 || d == b2) mask |= 1u << q;
     }
-    int64_t slot = wave_append(&list_count[b], pred);
-    if (pred) lp[slot] = key;
   }
+  int64_t slot = block_append(&list_count[b], (uint32_t)__popc(mask), s_wsum, &s_base);
+  uint32_t* lp = list + (int64_t)b * n + slot;
+#pragma unroll
+  for (int q = 0; q < kCollectPerThread; ++q)
+    if (mask & (1u << q)) *lp++ = keys[q];
 }
 
 // Resolve one rank within bucket `bk` (the key's top 12 bits) from the collected list.
@@ -120,8 +132,7 @@ void launch_median(const float* R, uint32_t* hist, MedianState* state, uint32_t*
                    unsigned long long* list_count, int B, int H, int W, hipStream_t st) {
   int64_t n = (int64_t)H * W;
   hipLaunchKernelGGL(k_med_scan, dim3(B), dim3(256), 0, st, hist, state, list_count, n);
-  int64_t blocks = (n + 255) / 256;
-  int gx = (int)(blocks < 2048 ? blocks : 2048);
+  int gx = (int)((n + 256 * kCollectPerThread - 1) / (256 * kCollectPerThread));
   hipLaunchKernelGGL(k_med_collect, dim3(gx, B), dim3(256), 0, st, R, state, list, list_count, n);
   hipLaunchKernelGGL(k_med_final, dim3(B), dim3(1024), 0, st, state, list, list_count, n);
 }

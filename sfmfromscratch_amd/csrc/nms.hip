@@ -49,22 +49,31 @@ __global__ void __launch_bounds__(256) k_nms(const float* __restrict__ R,
   const float med = st[b].median;
   const int c = tid & 63;
   const int rg = tid >> 6;
+  uint64_t keys[4];
+  bool flag[4];
+  uint32_t cnt = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int r = rg * 4 + q;
     const int gy = ty0 + r, gx = tx0 + c;
-    bool pred = false;
-    uint64_t key = 0;
+    flag[q] = false;
+    keys[q] = 0;
     if (gy < H && gx < W) {
       float m = s_m[r][c];
       for (int d = 1; d <= 2 * kh; ++d) m = fmaxf(m, s_m[r + d][c]);
       float v = s_r[r + kh][c + kh];
-      pred = (v < med) ? (v == 0.0f) : (v == m);
-      key = ((uint64_t)(~fkey(v)) << 32) | (uint32_t)(gy * W + gx);
+      flag[q] = (v < med) ? (v == 0.0f) : (v == m);
+      keys[q] = ((uint64_t)(~fkey(v)) << 32) | (uint32_t)(gy * W + gx);
     }
-    int64_t slot = wave_append(&cand_count[b], pred);
-    if (pred) cand[(int64_t)b * n + slot] = key;
+    cnt += flag[q] ? 1u : 0u;
   }
+  __shared__ uint32_t s_wsum[4];
+  __shared__ unsigned long long s_base;
+  int64_t slot = block_append(&cand_count[b], cnt, s_wsum, &s_base);
+  uint64_t* out = cand + (int64_t)b * n + slot;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (flag[q]) *out++ = keys[q];
 }
 
 void launch_nms(const float* R, const MedianState* state, uint64_t* cand,
