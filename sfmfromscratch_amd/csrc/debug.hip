@@ -58,29 +58,29 @@ int32_t sfm_debug_harris(int32_t device, const float* gauss, int32_t gs, double 
   int32_t rc = SFM_OK;
   if (hipMalloc(&d_img, n * 4) || hipMalloc(&d_R, n * 4) || hipMalloc(&d_g, 4 * gs * gs) ||
       hipMalloc(&d_hist, 4 * kHistBins) || hipMalloc(&d_list, n * 4) || hipMalloc(&d_med, sizeof(MedianState)) ||
-      hipMalloc(&d_cnt, 16) || hipMalloc(&d_cand, n * 8)) {
+      hipMalloc(&d_cnt, 16 * kCounterStride) || hipMalloc(&d_cand, n * 8)) {
     rc = SFM_EDEVICE;
   } else {
-    hipMemcpy(d_img, img, n * 4, hipMemcpyHostToDevice);
-    hipMemcpy(d_g, gauss, 4 * gs * gs, hipMemcpyHostToDevice);
-    hipMemset(d_hist, 0, 4 * kHistBins);
-    hipMemset(d_cnt, 0, 16);
+    (void)hipMemcpy(d_img, img, n * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_g, gauss, 4 * gs * gs, hipMemcpyHostToDevice);
+    (void)hipMemset(d_hist, 0, 4 * kHistBins);
+    (void)hipMemset(d_cnt, 0, 16 * kCounterStride);
     launch_harris(d_img, d_R, d_hist, 1, H, W, d_g, gs, (float)alpha, 0);
     launch_median(d_R, d_hist, d_med, d_list, d_cnt, 1, H, W, 0);
-    launch_nms(d_R, d_med, d_cand, d_cnt + 1, 1, H, W, ksize, 0);
+    launch_nms(d_R, d_med, d_cand, d_cnt + kCounterStride, 1, H, W, ksize, 0);
     MedianState ms;
-    unsigned long long cnt[2];
+    unsigned long long cnt[2 * kCounterStride];
     if (hipDeviceSynchronize() || hipMemcpy(R_out, d_R, n * 4, hipMemcpyDeviceToHost) ||
         hipMemcpy(&ms, d_med, sizeof(ms), hipMemcpyDeviceToHost) ||
-        hipMemcpy(cnt, d_cnt, 16, hipMemcpyDeviceToHost)) {
+        hipMemcpy(cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost)) {
       rc = SFM_EDEVICE;
     } else {
       *median_out = ms.median;
-      *ncand_out = (int64_t)cnt[1];
+      *ncand_out = (int64_t)cnt[kCounterStride];
     }
   }
-  hipFree(d_img); hipFree(d_R); hipFree(d_g); hipFree(d_hist); hipFree(d_list); hipFree(d_med);
-  hipFree(d_cnt); hipFree(d_cand);
+  void* bufs[] = {d_img, d_R, d_g, d_hist, d_list, d_med, d_cnt, d_cand};
+  for (void* b : bufs) (void)hipFree(b);
   return rc;
 }
 

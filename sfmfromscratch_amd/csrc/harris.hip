@@ -10,6 +10,8 @@
 // differently and move keypoints), accumulated per pixel as an fma chain
 // in row-major tap order (OpenCV FilterVec_32f's v_muladd chain).
 // VALU-bound by design.
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace sfm {
@@ -20,25 +22,25 @@ constexpr int kHT_H = 32;
 template <int KS>
 __global__ void __launch_bounds__(256) k_harris(const float* __restrict__ lvl, float* __restrict__ Rout,
                                                 uint32_t* __restrict__ hist_g, int H, int W,
-                                                int tiles_x, const float* __restrict__ gk,
-                                                float alpha) {
+                                                int tiles_x, int ntiles,
+                                                const float* __restrict__ gk, float alpha) {
   constexpr int GA = KS / 2;
   constexpr int PW = kHT_W + KS - 1;
   constexpr int PH = kHT_H + KS - 1;
   constexpr int IW = PW + 2;
   constexpr int IH = PH + 2;
-  constexpr int UN = (IH * IW > kHistBins) ? IH * IW : kHistBins;
   __shared__ float s_prod[3][PH][PW];
-  __shared__ float s_u[UN];  // image tile, then reused as the digit histogram
-  float* s_img = s_u;
-  uint32_t* s_hist = reinterpret_cast<uint32_t*>(s_u);
+  __shared__ float s_img[IH * IW];
+  __shared__ uint32_t s_hist[kHistBins];  // digit-1 histogram, flushed once per workgroup
 
   const int tid = threadIdx.x;
   const int b = blockIdx.y;
-  const int tile = blockIdx.x;
+  const float* img = lvl + (int64_t)b * H * W;
+  for (int i = tid; i < kHistBins; i += 256) s_hist[i] = 0u;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const int tx0 = (tile % tiles_x) * kHT_W;
   const int ty0 = (tile / tiles_x) * kHT_H;
-  const float* img = lvl + (int64_t)b * H * W;
+  __syncthreads();  // previous tile's LDS reads are done
 
   // 1. image tile with zero border (BORDER_CONSTANT)
   for (int idx = tid; idx < IH * IW; idx += 256) {
@@ -83,8 +85,6 @@ __global__ void __launch_bounds__(256) k_harris(const float* __restrict__ lvl, f
     s_prod[1][py][px] = pyy;
     s_prod[2][py][px] = pxy;
   }
-  __syncthreads();
-  for (int i = tid; i < kHistBins; i += 256) s_hist[i] = 0u;
   __syncthreads();
 
   // 3. window sums: thread owns columns 4*tq .. 4*tq+3 of rows ry and ry+16; the three
@@ -137,6 +137,7 @@ __global__ void __launch_bounds__(256) k_harris(const float* __restrict__ lvl, f
       }
     }
   }
+  }  // tile loop
   __syncthreads();
   uint32_t* hg = hist_g + (int64_t)b * kHistBins;
   for (int i = tid; i < kHistBins; i += 256) {
@@ -150,8 +151,12 @@ static void launch_ks(const float* lvl, float* R, uint32_t* hist, int B, int H, 
                       const float* gk, float alpha, hipStream_t st) {
   int tiles_x = (W + kHT_W - 1) / kHT_W;
   int tiles_y = (H + kHT_H - 1) / kHT_H;
-  hipLaunchKernelGGL(k_harris<KS>, dim3(tiles_x * tiles_y, B), dim3(256), 0, st, lvl, R, hist, H, W,
-                     tiles_x, gk, alpha);
+  int ntiles = tiles_x * tiles_y;
+  // ~4 resident workgroups per CU over the whole batch; each loops over tiles so the
+  // digit histogram is flushed once per workgroup instead of once per tile
+  int per_plane = std::max(1, std::min(ntiles, 512 / std::max(B, 1)));
+  hipLaunchKernelGGL(k_harris<KS>, dim3(per_plane, B), dim3(256), 0, st, lvl, R, hist, H, W, tiles_x,
+                     ntiles, gk, alpha);
 }
 
 void launch_harris(const float* lvl, float* R, uint32_t* hist, int B, int H, int W,

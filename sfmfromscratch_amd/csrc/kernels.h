@@ -18,6 +18,7 @@ constexpr int kHistBits = 12;               // first radix digit of the median s
 constexpr int kHistBins = 1 << kHistBits;   // 4096
 constexpr int kTopkLdsCap = 8192;           // max keys sorted in LDS by the top-k kernel
 constexpr int kMaxMatchRows = 16384;        // max keypoints per image for the matcher sort
+constexpr int kCounterStride = 32;          // u64 per per-plane atomic counter (own 256-B line)
 
 // Per-plane state of the exact median (np.median, NaiveSIFT.py:91).
 struct MedianState {
@@ -82,5 +83,13 @@ void launch_match_compact(const RowBest* rows, const int32_t* count, const int32
                           int max_rows, int64_t cap, int32_t* matches, float* conf, int32_t* nmatch,
                           hipStream_t st);
 void init_match_attributes(int max_rows);
+// match_mfma.hip: exact matching with the split-fp16 MFMA prefilter
+void launch_match_prep(const float* desc, const int32_t* count, int nimg, int64_t cap, int64_t capP,
+                       _Float16* hi, _Float16* lo, float* norm2, float* rnorm, unsigned int* imgmax,
+                       hipStream_t st);
+void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int64_t capP,
+                       const _Float16* hi, const _Float16* lo, const float* norm2, const float* rnorm,
+                       const unsigned int* imgmax, const int32_t* pairs, int P, float ratio,
+                       RowBest* rows, int max_rows, hipStream_t st);
 
 }  // namespace sfm

@@ -1,0 +1,283 @@
+// match_mfma.hip — exact NN-ratio matching with an MFMA prefilter.
+//
+// The reference's distances (NNRatioFeatureMatcher.py:31-34) are float32 pairwise sums;
+// its result only depends on, per query row, the two smallest distances and the argmin.
+// Those are found EXACTLY in three steps inside one workgroup of 128 query rows:
+//   1. approximate d^2 = |a|^2 + |b|^2 - 2 a.b for every target with fp16 split operands
+//      (a = hi + lo * 2^-11, three f16 MFMA products hi.hi + (hi.lo + lo.hi), f32
+//      accumulation, operands pre-scaled by 2^8 to keep them out of the f16 subnormal
+//      range) and keep each row's second-smallest approximate value D2~;
+//   2. sweep again and collect every target with d~ <= D2~ + 2 E_i, where E_i bounds
+//      |d~ - d_ref| rigorously (fp16 representation, dropped lo.lo term, f32 accumulation
+//      error <= K u sum|ab|, f32 rounding of d~ and of the reference's own pairwise sum);
+//      any target outside the window is strictly farther than the second nearest;
+//   3. recompute the collected candidates with the reference's exact float32 pairwise
+//      order (8 accumulators) and take (distance, index) minima -> ratio test.
+// Rows whose window overflows the per-row candidate list are recomputed exactly over
+// all targets (rare: only for runs of near-identical target descriptors).
+#include "kernels.h"
+
+namespace sfm {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kQW = 32;                // query rows per wave
+constexpr int kWaves = 4;              // waves per workgroup
+constexpr int kQB = kQW * kWaves;      // 128 query rows per workgroup
+constexpr int kTT = 32;                // targets per LDS tile
+constexpr int kRowH = 128 + 8;         // padded fp16 row in LDS (272 B): conflict-free b128 reads
+constexpr int kCandCap = 32;           // exact re-rank candidates per query row
+constexpr float kScale = 256.0f;       // operand pre-scale (2^8)
+constexpr float kLoScale = 2048.0f;    // lo part scale (2^11)
+
+// Per image: fp16 hi / lo (scaled) copies, squared norms (float32 of the float64 sum),
+// norms, and per-image maxima for the error bound.
+__global__ void __launch_bounds__(64) k_match_prep(const float* __restrict__ desc,
+                                                   const int32_t* __restrict__ count, int64_t cap,
+                                                   int64_t capP, _Float16* __restrict__ hi,
+                                                   _Float16* __restrict__ lo,
+                                                   float* __restrict__ norm2,
+                                                   float* __restrict__ rnorm,
+                                                   unsigned int* __restrict__ imgmax) {
+  const int img = blockIdx.y;
+  const int row = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int n = count[img];
+  const int64_t o = ((int64_t)img * capP + row) * 128;
+  float a0 = 0.0f, a1 = 0.0f;
+  if (row < n) {
+    const float* src = desc + ((int64_t)img * cap + row) * 128;
+    a0 = src[lane];
+    a1 = src[lane + 64];
+  }
+  float v[2] = {a0, a1};
+  double s = 0.0;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    float x = v[q] * kScale;
+    _Float16 h = (_Float16)x;
+    float r = (x - (float)h) * kLoScale;  // exact difference, exact power-of-two scaling
+    hi[o + lane + 64 * q] = h;
+    lo[o + lane + 64 * q] = (_Float16)r;
+    s += (double)v[q] * (double)v[q];
+  }
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) {
+    float n2 = (float)s;
+    float rn = (float)sqrt(s);
+    norm2[(int64_t)img * capP + row] = n2;
+    rnorm[(int64_t)img * capP + row] = rn;
+    if (row < n) {
+      atomicMax(&imgmax[img * 2 + 0], __float_as_uint(n2));  // positive floats order as uints
+      atomicMax(&imgmax[img * 2 + 1], __float_as_uint(rn));
+    }
+  }
+}
+
+// Reference-order exact squared distance (numpy pairwise, 8 accumulators).
+SFM_DEV float exact_sqdist(const float* __restrict__ a, const float* __restrict__ b) {
+  float r[8];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    float4 a0 = *reinterpret_cast<const float4*>(a + 8 * i);
+    float4 a1 = *reinterpret_cast<const float4*>(a + 8 * i + 4);
+    float4 b0 = *reinterpret_cast<const float4*>(b + 8 * i);
+    float4 b1 = *reinterpret_cast<const float4*>(b + 8 * i + 4);
+    float d[8] = {a0.x - b0.x, a0.y - b0.y, a0.z - b0.z, a0.w - b0.w,
+                  a1.x - b1.x, a1.y - b1.y, a1.z - b1.z, a1.w - b1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float sq = d[j] * d[j];
+      r[j] = (i == 0) ? sq : r[j] + sq;
+    }
+  }
+  float t01 = r[0] + r[1], t23 = r[2] + r[3], t45 = r[4] + r[5], t67 = r[6] + r[7];
+  float u0 = t01 + t23, u1 = t45 + t67;
+  return u0 + u1;
+}
+
+SFM_DEV void top2_merge(float& b1, int& j1, float& b2, float ob1, int oj1, float ob2) {
+  if (ob1 < b1 || (ob1 == b1 && oj1 < j1)) {
+    b2 = fminf(b1, ob2);
+    b1 = ob1;
+    j1 = oj1;
+  } else {
+    b2 = fminf(b2, ob1);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_match_mfma(
+    const float* __restrict__ desc, const int32_t* __restrict__ count, int64_t cap, int64_t capP,
+    const _Float16* __restrict__ hi, const _Float16* __restrict__ lo, const float* __restrict__ norm2,
+    const float* __restrict__ rnorm, const unsigned int* __restrict__ imgmax,
+    const int32_t* __restrict__ pairs, float ratio, RowBest* __restrict__ rows_out, int max_rows) {
+  __shared__ __attribute__((aligned(16))) _Float16 sHi[kTT][kRowH];
+  __shared__ __attribute__((aligned(16))) _Float16 sLo[kTT][kRowH];
+  __shared__ float sN[kTT];
+  __shared__ uint16_t sCand[kQB][kCandCap];
+  __shared__ float sDex[kQB][kCandCap];
+  __shared__ int sCnt[kQB];
+  __shared__ float sRed[3][256];
+  __shared__ int sRedJ[256];
+
+  const int p = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
+  const int n1 = count[i1], n2 = count[i2];
+  const int row0 = blockIdx.x * kQB;
+  if (row0 >= n1 || n2 < 1) return;
+
+  // this lane's query row (column of the MFMA output) and its fragments, kept in registers
+  const int ql = wid * kQW + (lane & 31);           // local query row 0..127
+  const int qi = row0 + ql;                          // query row in image i1
+  const int half = lane >> 5;
+  const int64_t qo = ((int64_t)i1 * capP + qi) * 128;
+  h8 qhi[8], qlo[8];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    qhi[kk] = *reinterpret_cast<const h8*>(hi + qo + kk * 16 + 8 * half);
+    qlo[kk] = *reinterpret_cast<const h8*>(lo + qo + kk * 16 + 8 * half);
+  }
+  const float na = norm2[(int64_t)i1 * capP + qi];
+  const float ra = rnorm[(int64_t)i1 * capP + qi];
+  const float maxn2 = __uint_as_float(imgmax[i2 * 2 + 0]);
+  const float maxrn = __uint_as_float(imgmax[i2 * 2 + 1]);
+  // rigorous |d~ - d_ref| bound (DESIGN.md §Matcher prefilter)
+  const float E = 3.0517578125e-05f * ra * maxrn + 4e-6f * (na + maxn2) + 1.25e-4f;
+  for (int i = tid; i < kQB; i += 256) sCnt[i] = 0;
+
+  const int ntiles = (n2 + kTT - 1) / kTT;
+  const int64_t to = (int64_t)i2 * capP * 128;
+  float thr = INFINITY;
+  for (int pass = 0; pass < 2; ++pass) {
+    float b1 = INFINITY, b2 = INFINITY;
+    for (int t = 0; t < ntiles; ++t) {
+      __syncthreads();
+      {  // stage 32 target rows (hi + lo) into LDS: 4 x 16 B per thread
+        const int r = tid >> 3, c = (tid & 7) * 16;
+        const int64_t g = to + (int64_t)(t * kTT + r) * 128 + c;
+        *reinterpret_cast<h8*>(&sHi[r][c]) = *reinterpret_cast<const h8*>(hi + g);
+        *reinterpret_cast<h8*>(&sHi[r][c + 8]) = *reinterpret_cast<const h8*>(hi + g + 8);
+        *reinterpret_cast<h8*>(&sLo[r][c]) = *reinterpret_cast<const h8*>(lo + g);
+        *reinterpret_cast<h8*>(&sLo[r][c + 8]) = *reinterpret_cast<const h8*>(lo + g + 8);
+        if (tid < kTT) sN[tid] = norm2[(int64_t)i2 * capP + t * kTT + tid];
+      }
+      __syncthreads();
+      f32x16 ahh = {}, ax = {};
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const h8 thi = *reinterpret_cast<const h8*>(&sHi[lane & 31][kk * 16 + 8 * half]);
+        const h8 tlo = *reinterpret_cast<const h8*>(&sLo[lane & 31][kk * 16 + 8 * half]);
+        ahh = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qhi[kk], ahh, 0, 0, 0);
+        ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qlo[kk], ax, 0, 0, 0);
+        ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(tlo, qhi[kk], ax, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int jl = (r & 3) + 8 * (r >> 2) + 4 * half;   // target row within the tile
+        const int j = t * kTT + jl;
+        const float s = (ahh[r] + ax[r] * (1.0f / kLoScale)) * (1.0f / (kScale * kScale));
+        const float t2 = na + sN[jl];
+        const float d = t2 - 2.0f * s;
+        if (j < n2) {
+          if (pass == 0) {
+            if (d < b1) { b2 = b1; b1 = d; }
+            else if (d < b2) b2 = d;
+          } else if (d <= thr && qi < n1) {
+            int slot = atomicAdd(&sCnt[ql], 1);
+            if (slot < kCandCap) sCand[ql][slot] = (uint16_t)j;
+          }
+        }
+      }
+    }
+    if (pass == 0) {
+      // merge the two lanes (halves) that share this query row
+      float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
+      float nb1 = fminf(b1, ob1);
+      float nb2 = fminf(fmaxf(b1, ob1), fminf(b2, ob2));
+      thr = nb2 + 2.0f * E;
+      (void)nb1;
+    }
+  }
+  __syncthreads();
+
+  // exact re-rank of the collected candidates
+  int maxc = 0;
+  for (int i = 0; i < kQB; ++i) maxc = max(maxc, min(sCnt[i], kCandCap));
+  const float* A = desc + (int64_t)i1 * cap * 128;
+  const float* Bd = desc + (int64_t)i2 * cap * 128;
+  for (int idx = tid; idx < kQB * maxc; idx += 256) {
+    const int rl = idx % kQB, slot = idx / kQB;
+    const int c = sCnt[rl];
+    if (slot < c && c <= kCandCap && row0 + rl < n1)
+      sDex[rl][slot] = exact_sqdist(A + (int64_t)(row0 + rl) * 128, Bd + (int64_t)sCand[rl][slot] * 128);
+  }
+  __syncthreads();
+  if (tid < kQB && row0 + tid < n1 && sCnt[tid] <= kCandCap) {
+    float b1 = INFINITY, b2 = INFINITY;
+    int j1 = 0x7fffffff;
+    const int c = sCnt[tid];
+    for (int s = 0; s < c; ++s) {
+      const float d = sDex[tid][s];
+      const int j = sCand[tid][s];
+      if (d < b1 || (d == b1 && j < j1)) { b2 = b1; b1 = d; j1 = j; }
+      else if (d < b2) b2 = d;
+    }
+    RowBest rb;
+    rb.col = -1;
+    rb.nndr = 0.0f;
+    const float d1 = sqrtf(b1), d2 = sqrtf(b2);
+    if (d2 > 0.0f) {
+      const float nndr = d1 / d2;
+      if (nndr <= ratio) { rb.col = j1; rb.nndr = nndr; }
+    }
+    rows_out[(int64_t)p * max_rows + row0 + tid] = rb;
+  }
+  // overflow rows: exact over every target (whole workgroup per row)
+  for (int rl = 0; rl < kQB; ++rl) {
+    if (sCnt[rl] <= kCandCap || row0 + rl >= n1) continue;  // uniform branch
+    float b1 = INFINITY, b2 = INFINITY;
+    int j1 = 0x7fffffff;
+    for (int j = tid; j < n2; j += 256) {
+      const float d = exact_sqdist(A + (int64_t)(row0 + rl) * 128, Bd + (int64_t)j * 128);
+      if (d < b1 || (d == b1 && j < j1)) { b2 = b1; b1 = d; j1 = j; }
+      else if (d < b2) b2 = d;
+    }
+    sRed[0][tid] = b1; sRed[1][tid] = b2; sRedJ[tid] = j1;
+    __syncthreads();
+    if (tid == 0) {
+      float B1 = INFINITY, B2 = INFINITY;
+      int J1 = 0x7fffffff;
+      for (int t = 0; t < 256; ++t) top2_merge(B1, J1, B2, sRed[0][t], sRedJ[t], sRed[1][t]);
+      RowBest rb;
+      rb.col = -1;
+      rb.nndr = 0.0f;
+      const float d1 = sqrtf(B1), d2 = sqrtf(B2);
+      if (d2 > 0.0f) {
+        const float nndr = d1 / d2;
+        if (nndr <= ratio) { rb.col = J1; rb.nndr = nndr; }
+      }
+      rows_out[(int64_t)p * max_rows + row0 + rl] = rb;
+    }
+    __syncthreads();
+  }
+}
+
+void launch_match_prep(const float* desc, const int32_t* count, int nimg, int64_t cap, int64_t capP,
+                       _Float16* hi, _Float16* lo, float* norm2, float* rnorm, unsigned int* imgmax,
+                       hipStream_t st) {
+  (void)hipMemsetAsync(imgmax, 0, (size_t)nimg * 2 * sizeof(unsigned int), st);
+  hipLaunchKernelGGL(k_match_prep, dim3((unsigned)capP, nimg), dim3(64), 0, st, desc, count, cap, capP, hi,
+                     lo, norm2, rnorm, imgmax);
+}
+
+void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int64_t capP,
+                       const _Float16* hi, const _Float16* lo, const float* norm2, const float* rnorm,
+                       const unsigned int* imgmax, const int32_t* pairs, int P, float ratio,
+                       RowBest* rows, int max_rows, hipStream_t st) {
+  hipLaunchKernelGGL(k_match_mfma, dim3((max_rows + kQB - 1) / kQB, P), dim3(256), 0, st, desc, count, cap,
+                     capP, hi, lo, norm2, rnorm, imgmax, pairs, ratio, rows, max_rows);
+}
+
+}  // namespace sfm

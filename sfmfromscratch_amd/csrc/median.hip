@@ -33,7 +33,7 @@ __global__ void __launch_bounds__(256) k_med_scan(const uint32_t* __restrict__ h
     st[b].rank[0] = r1;
     st[b].rank[1] = r2;
     st[b].odd = (uint32_t)(n % 2);
-    list_count[b] = 0ull;
+    list_count[(int64_t)b * kCounterStride] = 0ull;
   }
 }
 
@@ -65,7 +65,8 @@ __global__ void __launch_bounds__(256) k_med_collect(const float* __restrict__ R
       if (d == b1 || d == b2) mask |= 1u << q;
     }
   }
-  int64_t slot = block_append(&list_count[b], (uint32_t)__popc(mask), s_wsum, &s_base);
+  int64_t slot = block_append(&list_count[(int64_t)b * kCounterStride], (uint32_t)__popc(mask), s_wsum,
+                              &s_base);
   uint32_t* lp = list + (int64_t)b * n + slot;
 #pragma unroll
   for (int q = 0; q < kCollectPerThread; ++q)
@@ -112,7 +113,7 @@ __global__ void __launch_bounds__(1024) k_med_final(MedianState* __restrict__ st
   __shared__ uint32_t s_out[2];
   const int b = blockIdx.x;
   const uint32_t* lp = list + (int64_t)b * n;
-  const int64_t m = (int64_t)list_count[b];
+  const int64_t m = (int64_t)list_count[(int64_t)b * kCounterStride];
   MedianState s = st[b];
   uint32_t key1 = select_in_list(lp, m, s.bucket[0], s.rank[0], s_h, s_scan, s_out);
   float v1 = fkey_inv(key1);

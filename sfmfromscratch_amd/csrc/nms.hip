@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(256) k_nms(const float* __restrict__ R,
   }
   __shared__ uint32_t s_wsum[4];
   __shared__ unsigned long long s_base;
-  int64_t slot = block_append(&cand_count[b], cnt, s_wsum, &s_base);
+  int64_t slot = block_append(&cand_count[(int64_t)b * kCounterStride], cnt, s_wsum, &s_base);
   uint64_t* out = cand + (int64_t)b * n + slot;
 #pragma unroll
   for (int q = 0; q < 4; ++q)

@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(1024) k_topk(const uint64_t* __restrict__ cand
   const int b = blockIdx.x;
   const int64_t n = (int64_t)H * W;
   const uint64_t* cp = cand + (int64_t)b * n;
-  const int64_t C = (int64_t)cand_count[b];
+  const int64_t C = (int64_t)cand_count[(int64_t)b * kCounterStride];
   const int kk = (int)((int64_t)k < C ? (int64_t)k : C);
   if (kk <= 0) {
     if (tid == 0) kp.count[b] = 0;

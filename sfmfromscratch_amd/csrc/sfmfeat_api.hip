@@ -10,6 +10,7 @@
 //           -> per-pair compaction + (nndr, row) sort.
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -47,6 +48,8 @@ struct sfm_ctx {
   DevBuf d_gauss, d_img0, d_lvl, d_R, d_hist, d_med, d_medlist, d_counts, d_cand, d_scratch,
       d_kpx, d_kpy, d_kpc, d_lc, d_xy, d_desc, d_conf, d_count, d_u8;
   DevBuf m_desc, m_count, m_pairs, m_descT, m_rows, m_matches, m_conf, m_nmatch;
+  DevBuf m_hi, m_lo, m_norm2, m_rnorm, m_imgmax;
+  bool match_direct = false;  // SFMFEAT_MATCH_DIRECT=1: all-pairs exact VALU kernel (A/B checks)
   // stage profiling (sfm_profile_*): HIP events bracketing each stage's launches
   bool prof = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
@@ -192,7 +195,7 @@ int reserve_impl(sfm_ctx* c, int B, int H, int W) {
   if ((rc = ensure(c, c->d_hist, (size_t)c->L * B * kHistBins * 4))) return rc;
   if ((rc = ensure(c, c->d_med, (size_t)c->L * B * sizeof(MedianState)))) return rc;
   if ((rc = ensure(c, c->d_medlist, (size_t)B * A0 * 4))) return rc;
-  if ((rc = ensure(c, c->d_counts, (size_t)2 * c->L * B * 8))) return rc;
+  if ((rc = ensure(c, c->d_counts, (size_t)2 * c->L * B * 8 * kCounterStride))) return rc;
   if ((rc = ensure(c, c->d_cand, (size_t)B * A0 * 8))) return rc;
   if ((rc = ensure(c, c->d_scratch, (size_t)B * A0 * 8))) return rc;
   size_t nk = (size_t)c->L * B * (size_t)std::max(c->kcap, 1);
@@ -227,9 +230,9 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     }
   }
   HIPCHK(c, hipMemsetAsync(c->d_hist.p, 0, (size_t)L * B * kHistBins * 4, st));
-  HIPCHK(c, hipMemsetAsync(c->d_counts.p, 0, (size_t)2 * L * B * 8, st));
+  HIPCHK(c, hipMemsetAsync(c->d_counts.p, 0, (size_t)2 * L * B * 8 * kCounterStride, st));
   unsigned long long* medcnt = as<unsigned long long>(c->d_counts);
-  unsigned long long* candcnt = medcnt + (size_t)L * B;
+  unsigned long long* candcnt = medcnt + (size_t)L * B * kCounterStride;
   const float alpha = (float)c->p.alpha;  // NEP 50: the python float becomes float32
   for (int l = 0; l < L; ++l) {
     const int h = lv[l].h, w = lv[l].w;
@@ -242,12 +245,12 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     }
     {
       StageScope sc(c, SFM_PROF_MEDIAN, st);
-      launch_median(as<float>(c->d_R), hist, med, as<uint32_t>(c->d_medlist), medcnt + (size_t)l * B, B,
+      launch_median(as<float>(c->d_R), hist, med, as<uint32_t>(c->d_medlist), medcnt + (size_t)l * B * kCounterStride, B,
                     h, w, st);
     }
     {
       StageScope sc(c, SFM_PROF_NMS, st);
-      launch_nms(as<float>(c->d_R), med, as<uint64_t>(c->d_cand), candcnt + (size_t)l * B, B, h, w,
+      launch_nms(as<float>(c->d_R), med, as<uint64_t>(c->d_cand), candcnt + (size_t)l * B * kCounterStride, B, h, w,
                  c->p.ksize, st);
     }
     KpList kp;
@@ -257,7 +260,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     kp.conf = as<float>(c->d_kpc) + ko;
     kp.count = as<int32_t>(c->d_lc) + (size_t)l * B;
     StageScope sc(c, SFM_PROF_TOPK, st);
-    launch_topk(as<uint64_t>(c->d_cand), candcnt + (size_t)l * B, as<uint64_t>(c->d_scratch), kp,
+    launch_topk(as<uint64_t>(c->d_cand), candcnt + (size_t)l * B * kCounterStride, as<uint64_t>(c->d_scratch), kp,
                 std::max(c->kcap, 1), c->kcap, B, h, w, lv[l].fw / 2, st);
   }
   const int rotate = c->p.mode == SFM_MODE_NAIVE ? 0 : 1;
@@ -283,18 +286,39 @@ int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, in
   if (P <= 0) return SFM_OK;
   if (cap < 1 || cap > kMaxMatchRows)
     return set_err(c, SFM_EINVAL, "match capacity must be in [1, 16384]");
-  int64_t capP = (cap + 63) / 64 * 64;
   int rc;
-  if ((rc = ensure(c, c->m_descT, (size_t)nimg * 128 * capP * 4))) return rc;
-  if ((rc = ensure(c, c->m_rows, (size_t)P * cap * sizeof(RowBest)))) return rc;
-  {
-    StageScope sc(c, SFM_PROF_MATCH_PREP, st);
-    launch_transpose_desc(desc, count, nimg, cap, capP, as<float>(c->m_descT), st);
-  }
-  {
-    StageScope sc(c, SFM_PROF_MATCH, st);
-    launch_match_rows(as<float>(c->m_descT), count, capP, pairs, P, ratio, as<RowBest>(c->m_rows),
-                      (int)cap, st);
+  if (c->match_direct) {
+    int64_t capP = (cap + 63) / 64 * 64;
+    if ((rc = ensure(c, c->m_descT, (size_t)nimg * 128 * capP * 4))) return rc;
+    if ((rc = ensure(c, c->m_rows, (size_t)P * cap * sizeof(RowBest)))) return rc;
+    {
+      StageScope sc(c, SFM_PROF_MATCH_PREP, st);
+      launch_transpose_desc(desc, count, nimg, cap, capP, as<float>(c->m_descT), st);
+    }
+    {
+      StageScope sc(c, SFM_PROF_MATCH, st);
+      launch_match_rows(as<float>(c->m_descT), count, capP, pairs, P, ratio, as<RowBest>(c->m_rows),
+                        (int)cap, st);
+    }
+  } else {
+    int64_t capP = (cap + 127) / 128 * 128;
+    if ((rc = ensure(c, c->m_hi, (size_t)nimg * capP * 128 * 2))) return rc;
+    if ((rc = ensure(c, c->m_lo, (size_t)nimg * capP * 128 * 2))) return rc;
+    if ((rc = ensure(c, c->m_norm2, (size_t)nimg * capP * 4))) return rc;
+    if ((rc = ensure(c, c->m_rnorm, (size_t)nimg * capP * 4))) return rc;
+    if ((rc = ensure(c, c->m_imgmax, (size_t)nimg * 8))) return rc;
+    if ((rc = ensure(c, c->m_rows, (size_t)P * cap * sizeof(RowBest)))) return rc;
+    {
+      StageScope sc(c, SFM_PROF_MATCH_PREP, st);
+      launch_match_prep(desc, count, nimg, cap, capP, as<_Float16>(c->m_hi), as<_Float16>(c->m_lo),
+                        as<float>(c->m_norm2), as<float>(c->m_rnorm), as<unsigned int>(c->m_imgmax), st);
+    }
+    {
+      StageScope sc(c, SFM_PROF_MATCH, st);
+      launch_match_mfma(desc, count, cap, capP, as<_Float16>(c->m_hi), as<_Float16>(c->m_lo),
+                        as<float>(c->m_norm2), as<float>(c->m_rnorm), as<unsigned int>(c->m_imgmax), pairs,
+                        P, ratio, as<RowBest>(c->m_rows), (int)cap, st);
+    }
   }
   {
     StageScope sc(c, SFM_PROF_MATCH_POST, st);
@@ -368,6 +392,10 @@ int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out) {
     return SFM_EINVAL;
   }
   c->kcap = (int)k;
+  {
+    const char* e = getenv("SFMFEAT_MATCH_DIRECT");
+    c->match_direct = e && e[0] == '1';
+  }
   c->cap = (int64_t)c->L * k;
   int gs = p->gaussian_size;
   if (p->gauss_kernel_set) memcpy(c->gauss, p->gauss_kernel, sizeof(float) * gs * gs);
@@ -396,7 +424,8 @@ int32_t sfm_ctx_destroy(sfm_ctx* c) {
   DevBuf* bufs[] = {&c->d_gauss, &c->d_img0, &c->d_lvl, &c->d_R, &c->d_hist, &c->d_med, &c->d_medlist,
                     &c->d_counts, &c->d_cand, &c->d_scratch, &c->d_kpx, &c->d_kpy, &c->d_kpc, &c->d_lc,
                     &c->d_xy, &c->d_desc, &c->d_conf, &c->d_count, &c->d_u8, &c->m_desc, &c->m_count, &c->m_pairs,
-                    &c->m_descT, &c->m_rows, &c->m_matches, &c->m_conf, &c->m_nmatch};
+                    &c->m_descT, &c->m_rows, &c->m_matches, &c->m_conf, &c->m_nmatch,
+                    &c->m_hi, &c->m_lo, &c->m_norm2, &c->m_rnorm, &c->m_imgmax};
   for (DevBuf* b : bufs) free_buf(*b);
   for (auto& e : c->prof_pending) {
     (void)hipEventDestroy(e.second.first);

@@ -148,6 +148,23 @@ def test_matcher_vs_oracle_sizes(n1, n2, ratio):
         assert_matches_equal(om, oc, m, c)
 
 
+@pytest.mark.parametrize("n1,n2,jit,ratio", [(10, 700, 0, 0.9), (10, 700, 1, 0.9), (40, 900, 0, 1.0),
+                                             (300, 300, 0, 0.8)])
+def test_matcher_duplicate_targets_overflow_path(n1, n2, jit, ratio):
+    """Runs of identical / near-identical targets widen the prefilter window past the
+    per-row candidate list and exercise the exact full-row fallback."""
+    a, ha = synth.make_descriptor_table(n1, 7 + n1)
+    b, _ = synth.make_descriptor_table(n2, 9 + n2, dup_of=ha, jitter=jit)
+    q, _ = synth.make_descriptor_table(n1, 11 + n1, dup_of=ha, jitter=2)
+    for qq in (a, q):
+        m, c = NNRatioFeatureMatcher(ratio).match_features_ratio_test(qq, b)
+        om, oc = O.match(qq, b, ratio)
+        if len(oc) == 0:
+            assert m.shape == (0,)
+        else:
+            assert_matches_equal(om, oc, m, c)
+
+
 def test_matcher_index_error_and_empty():
     a, _ = synth.make_descriptor_table(4, 1)
     with pytest.raises(IndexError):
