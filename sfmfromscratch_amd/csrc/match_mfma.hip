@@ -33,16 +33,15 @@ constexpr float kLoScale = 2048.0f;    // lo part scale (2^11)
 
 // Per image: fp16 hi / lo (scaled) copies, squared norms (float32 of the float64 sum),
 // norms, and per-image maxima for the error bound.
-__global__ void __launch_bounds__(64) k_match_prep(const float* __restrict__ desc,
+__global__ void __launch_bounds__(256) k_match_prep(const float* __restrict__ desc,
                                                    const int32_t* __restrict__ count, int64_t cap,
                                                    int64_t capP, _Float16* __restrict__ hi,
                                                    _Float16* __restrict__ lo,
                                                    float* __restrict__ norm2,
-                                                   float* __restrict__ rnorm,
-                                                   unsigned int* __restrict__ imgmax) {
+                                                   float* __restrict__ rnorm) {
   const int img = blockIdx.y;
-  const int row = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per row
+  const int lane = threadIdx.x & 63;
   const int n = count[img];
   const int64_t o = ((int64_t)img * capP + row) * 128;
   float a0 = 0.0f, a1 = 0.0f;
@@ -68,10 +67,35 @@ __global__ void __launch_bounds__(64) k_match_prep(const float* __restrict__ des
     float rn = (float)sqrt(s);
     norm2[(int64_t)img * capP + row] = n2;
     rnorm[(int64_t)img * capP + row] = rn;
-    if (row < n) {
-      atomicMax(&imgmax[img * 2 + 0], __float_as_uint(n2));  // positive floats order as uints
-      atomicMax(&imgmax[img * 2 + 1], __float_as_uint(rn));
+  }
+}
+
+// Per-image maxima of the squared norms and norms (block reduction, no atomics).
+__global__ void __launch_bounds__(256) k_match_imgmax(const int32_t* __restrict__ count, int64_t capP,
+                                                      const float* __restrict__ norm2,
+                                                      const float* __restrict__ rnorm,
+                                                      unsigned int* __restrict__ imgmax) {
+  __shared__ float s_a[256], s_b[256];
+  const int img = blockIdx.x, tid = threadIdx.x;
+  const int n = count[img];
+  float a = 0.0f, b = 0.0f;
+  for (int r = tid; r < n; r += 256) {
+    a = fmaxf(a, norm2[(int64_t)img * capP + r]);
+    b = fmaxf(b, rnorm[(int64_t)img * capP + r]);
+  }
+  s_a[tid] = a;
+  s_b[tid] = b;
+  __syncthreads();
+  for (int off = 128; off >= 1; off >>= 1) {
+    if (tid < off) {
+      s_a[tid] = fmaxf(s_a[tid], s_a[tid + off]);
+      s_b[tid] = fmaxf(s_b[tid], s_b[tid + off]);
     }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    imgmax[img * 2 + 0] = __float_as_uint(s_a[0]);
+    imgmax[img * 2 + 1] = __float_as_uint(s_b[0]);
   }
 }
 
@@ -267,9 +291,9 @@ __global__ void __launch_bounds__(256) k_match_mfma(
 void launch_match_prep(const float* desc, const int32_t* count, int nimg, int64_t cap, int64_t capP,
                        _Float16* hi, _Float16* lo, float* norm2, float* rnorm, unsigned int* imgmax,
                        hipStream_t st) {
-  (void)hipMemsetAsync(imgmax, 0, (size_t)nimg * 2 * sizeof(unsigned int), st);
-  hipLaunchKernelGGL(k_match_prep, dim3((unsigned)capP, nimg), dim3(64), 0, st, desc, count, cap, capP, hi,
-                     lo, norm2, rnorm, imgmax);
+  hipLaunchKernelGGL(k_match_prep, dim3((unsigned)(capP / 4), nimg), dim3(256), 0, st, desc, count, cap, capP, hi,
+                     lo, norm2, rnorm);
+  hipLaunchKernelGGL(k_match_imgmax, dim3(nimg), dim3(256), 0, st, count, capP, norm2, rnorm, imgmax);
 }
 
 void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int64_t capP,

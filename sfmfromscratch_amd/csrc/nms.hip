@@ -14,16 +14,20 @@
 namespace sfm {
 
 constexpr int kNT_W = 64;
-constexpr int kNT_H = 16;
-constexpr int kMaxHalf = SFM_NMS_MAX_HALF;
+constexpr int kNT_H = 32;
+constexpr int kRowsPerThread = kNT_H / 4;  // 256 threads = 64 columns x 4 row groups
 
+template <int KH>  // KH = ksize // 2 (KH_MAX = SFM_NMS_MAX_HALF when instantiated generic)
 __global__ void __launch_bounds__(256) k_nms(const float* __restrict__ R,
                                              const MedianState* __restrict__ st,
                                              uint64_t* __restrict__ cand,
                                              unsigned long long* __restrict__ cand_count, int H,
                                              int W, int kh, int tiles_x) {
-  __shared__ float s_r[kNT_H + 2 * kMaxHalf][kNT_W + 2 * kMaxHalf];
-  __shared__ float s_m[kNT_H + 2 * kMaxHalf][kNT_W];
+  constexpr int KM = KH;  // LDS sized for the template half-width
+  __shared__ float s_r[kNT_H + 2 * KM][kNT_W + 2 * KM];
+  __shared__ float s_m[kNT_H + 2 * KM][kNT_W];
+  __shared__ uint32_t s_wsum[4];
+  __shared__ unsigned long long s_base;
   const int tid = threadIdx.x;
   const int b = blockIdx.y;
   const int tx0 = (blockIdx.x % tiles_x) * kNT_W;
@@ -34,7 +38,7 @@ __global__ void __launch_bounds__(256) k_nms(const float* __restrict__ R,
   for (int idx = tid; idx < THh * TWh; idx += 256) {
     int iy = idx / TWh, ix = idx - iy * TWh;
     int gy = ty0 - kh + iy, gx = tx0 - kh + ix;
-    float v = -INFINITY;
+    float v = -INFINITY;  // outside the image: never the (clipped) window max
     if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = Rp[(int64_t)gy * W + gx];
     s_r[iy][ix] = v;
   }
@@ -49,31 +53,31 @@ __global__ void __launch_bounds__(256) k_nms(const float* __restrict__ R,
   const float med = st[b].median;
   const int c = tid & 63;
   const int rg = tid >> 6;
-  uint64_t keys[4];
-  bool flag[4];
-  uint32_t cnt = 0;
+  uint32_t flags = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = rg * 4 + q;
+  for (int q = 0; q < kRowsPerThread; ++q) {
+    const int r = rg * kRowsPerThread + q;
     const int gy = ty0 + r, gx = tx0 + c;
-    flag[q] = false;
-    keys[q] = 0;
     if (gy < H && gx < W) {
       float m = s_m[r][c];
       for (int d = 1; d <= 2 * kh; ++d) m = fmaxf(m, s_m[r + d][c]);
-      float v = s_r[r + kh][c + kh];
-      flag[q] = (v < med) ? (v == 0.0f) : (v == m);
-      keys[q] = ((uint64_t)(~fkey(v)) << 32) | (uint32_t)(gy * W + gx);
+      const float v = s_r[r + kh][c + kh];
+      const bool pred = (v < med) ? (v == 0.0f) : (v == m);
+      flags |= pred ? (1u << q) : 0u;
     }
-    cnt += flag[q] ? 1u : 0u;
   }
-  __shared__ uint32_t s_wsum[4];
-  __shared__ unsigned long long s_base;
-  int64_t slot = block_append(&cand_count[(int64_t)b * kCounterStride], cnt, s_wsum, &s_base);
+  const int64_t slot = block_append(&cand_count[(int64_t)b * kCounterStride], (uint32_t)__popc(flags), s_wsum,
+                                    &s_base);
   uint64_t* out = cand + (int64_t)b * n + slot;
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (flag[q]) *out++ = keys[q];
+  for (int q = 0; q < kRowsPerThread; ++q) {
+    if (flags & (1u << q)) {
+      const int r = rg * kRowsPerThread + q;
+      const int gy = ty0 + r, gx = tx0 + c;
+      const float v = s_r[r + kh][c + kh];
+      *out++ = ((uint64_t)(~fkey(v)) << 32) | (uint32_t)(gy * W + gx);
+    }
+  }
 }
 
 void launch_nms(const float* R, const MedianState* state, uint64_t* cand,
@@ -81,8 +85,16 @@ void launch_nms(const float* R, const MedianState* state, uint64_t* cand,
   int kh = ksize / 2;
   int tiles_x = (W + kNT_W - 1) / kNT_W;
   int tiles_y = (H + kNT_H - 1) / kNT_H;
-  hipLaunchKernelGGL(k_nms, dim3(tiles_x * tiles_y, B), dim3(256), 0, st, R, state, cand, cand_count,
-                     H, W, kh, tiles_x);
+  dim3 grid(tiles_x * tiles_y, B);
+  switch (kh) {
+    case 0: hipLaunchKernelGGL(k_nms<0>, grid, dim3(256), 0, st, R, state, cand, cand_count, H, W, kh, tiles_x); break;
+    case 1: hipLaunchKernelGGL(k_nms<1>, grid, dim3(256), 0, st, R, state, cand, cand_count, H, W, kh, tiles_x); break;
+    case 2: hipLaunchKernelGGL(k_nms<2>, grid, dim3(256), 0, st, R, state, cand, cand_count, H, W, kh, tiles_x); break;
+    case 3: hipLaunchKernelGGL(k_nms<3>, grid, dim3(256), 0, st, R, state, cand, cand_count, H, W, kh, tiles_x); break;
+    default:
+      hipLaunchKernelGGL(k_nms<SFM_NMS_MAX_HALF>, grid, dim3(256), 0, st, R, state, cand, cand_count, H, W, kh, tiles_x);
+      break;
+  }
 }
 
 }  // namespace sfm
