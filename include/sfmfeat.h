@@ -192,6 +192,11 @@ int32_t sfm_debug_harris(int32_t device, const float* gauss, int32_t gs, double 
                          int32_t ksize, const float* img, int32_t H, int32_t W, float* R_out,
                          float* median_out, int64_t* ncand_out);
 
+/* Mean time (ms) of one fused Harris launch on synthetic planes, ablation variant abl
+ * (0 full, 1 no digit histogram, 2 no window sums, 3 no Sobel/products). */
+float sfm_debug_time_harris(int32_t device, int32_t abl, int32_t B, int32_t H, int32_t W,
+                            int32_t iters);
+
 #ifdef __cplusplus
 }
 #endif

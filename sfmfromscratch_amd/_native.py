@@ -49,6 +49,7 @@ SIGNATURES = {
                                              ctypes.c_float, _vp, _vp, _vp, _vp]),
     "sfm_profile_enable": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "sfm_profile_read": (ctypes.c_int32, [_vp, ctypes.POINTER(ctypes.c_double), _i64p, ctypes.c_int32]),
+    "sfm_debug_time_harris": (ctypes.c_float, [ctypes.c_int32] * 6),
     "sfm_debug_atan2": (ctypes.c_int32, [ctypes.c_int32, _fp, _fp, _fp, ctypes.c_int64]),
     "sfm_debug_harris": (ctypes.c_int32, [ctypes.c_int32, _fp, ctypes.c_int32, ctypes.c_double, ctypes.c_int32,
                                           _fp, ctypes.c_int32, ctypes.c_int32, _fp, _fp, _i64p]),

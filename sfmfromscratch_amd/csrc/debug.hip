@@ -57,13 +57,13 @@ int32_t sfm_debug_harris(int32_t device, const float* gauss, int32_t gs, double 
   uint64_t* d_cand = nullptr;
   int32_t rc = SFM_OK;
   if (hipMalloc(&d_img, n * 4) || hipMalloc(&d_R, n * 4) || hipMalloc(&d_g, 4 * gs * gs) ||
-      hipMalloc(&d_hist, 4 * kHistBins) || hipMalloc(&d_list, n * 4) || hipMalloc(&d_med, sizeof(MedianState)) ||
+      hipMalloc(&d_hist, 4 * kMedBins1) || hipMalloc(&d_list, n * 4) || hipMalloc(&d_med, sizeof(MedianState)) ||
       hipMalloc(&d_cnt, 16 * kCounterStride) || hipMalloc(&d_cand, n * 8)) {
     rc = SFM_EDEVICE;
   } else {
     (void)hipMemcpy(d_img, img, n * 4, hipMemcpyHostToDevice);
     (void)hipMemcpy(d_g, gauss, 4 * gs * gs, hipMemcpyHostToDevice);
-    (void)hipMemset(d_hist, 0, 4 * kHistBins);
+    (void)hipMemset(d_hist, 0, 4 * kMedBins1);
     (void)hipMemset(d_cnt, 0, 16 * kCounterStride);
     launch_harris(d_img, d_R, d_hist, 1, H, W, d_g, gs, (float)alpha, 0);
     launch_median(d_R, d_hist, d_med, d_list, d_cnt, 1, H, W, 0);
@@ -82,6 +82,33 @@ int32_t sfm_debug_harris(int32_t device, const float* gauss, int32_t gs, double 
   void* bufs[] = {d_img, d_R, d_g, d_hist, d_list, d_med, d_cnt, d_cand};
   for (void* b : bufs) (void)hipFree(b);
   return rc;
+}
+
+// Mean time (ms) of one k_harris<7> launch over B x H x W synthetic planes for ablation
+// variant `abl` (0 full, 1 no histogram, 2 no window sums, 3 no Sobel/products).
+float sfm_debug_time_harris(int32_t device, int32_t abl, int32_t B, int32_t H, int32_t W, int32_t iters) {
+  if (hipSetDevice(device) != hipSuccess) return -1.0f;
+  int64_t n = (int64_t)B * H * W;
+  float *d_img = nullptr, *d_R = nullptr, *d_g = nullptr;
+  uint32_t* d_hist = nullptr;
+  if (hipMalloc(&d_img, n * 4) || hipMalloc(&d_R, n * 4) || hipMalloc(&d_g, 4 * 49) ||
+      hipMalloc(&d_hist, (size_t)B * 4 * kMedBins1))
+    return -1.0f;
+  std::vector<float> h(n);
+  uint32_t x = 12345u;
+  for (int64_t i = 0; i < n; ++i) {
+    x = x * 1664525u + 1013904223u;
+    h[i] = (float)(x >> 24) / 255.0f;
+  }
+  float g[49];
+  for (int i = 0; i < 49; ++i) g[i] = 1.0f / 49.0f;
+  (void)hipMemcpy(d_img, h.data(), n * 4, hipMemcpyHostToDevice);
+  (void)hipMemcpy(d_g, g, 4 * 49, hipMemcpyHostToDevice);
+  (void)hipMemset(d_hist, 0, (size_t)B * 4 * kMedBins1);
+  float ms = time_harris_ablation(abl, d_img, d_R, d_hist, B, H, W, d_g, 0.05f, iters);
+  void* bufs[] = {d_img, d_R, d_g, d_hist};
+  for (void* b : bufs) (void)hipFree(b);
+  return ms;
 }
 
 }  // extern "C"

@@ -15,7 +15,9 @@ namespace sfm {
 #define SFM_NMS_MAX_HALF 15                 // ksize <= 31
 
 constexpr int kHistBits = 12;               // first radix digit of the median select
-constexpr int kHistBins = 1 << kHistBits;   // 4096
+constexpr int kHistBins = 1 << kHistBits;   // 4096: generic LDS histogram for <= 12-bit digits
+constexpr int kMedBits1 = 11;               // median digit 1 (histogrammed inside Harris)
+constexpr int kMedBins1 = 1 << kMedBits1;   // 2048 (digits 2 / 3 are 11 / 10 bits)
 constexpr int kTopkLdsCap = 8192;           // max keys sorted in LDS by the top-k kernel
 constexpr int kMaxMatchRows = 16384;        // max keypoints per image for the matcher sort
 constexpr int kCounterStride = 32;          // u64 per per-plane atomic counter (own 256-B line)
@@ -44,6 +46,9 @@ void launch_resize(const float* src, int sh, int sw, float* dst, int dh, int dw,
 // harris.hip: R map + first median digit histogram (hist zeroed by the caller).
 void launch_harris(const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
                    const float* d_gauss, int ks, float alpha, hipStream_t st);
+
+float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
+                           const float* gk, float alpha, int iters);
 
 // median.hip
 void launch_median(const float* R, uint32_t* hist, MedianState* state, uint32_t* list,

@@ -2,7 +2,7 @@
 // order-preserving 32-bit keys of the float32 values.
 //   even H*W: float32 (v[k1] + v[k2]) / 2 with k1 = n/2-1, k2 = n/2
 //   odd  H*W: v[n/2]
-// Digit 1 (top 12 bits) is histogrammed inside the Harris kernel.  Then:
+// Digit 1 (top 11 bits) is histogrammed inside the Harris kernel.  Then:
 //   k_med_scan    : one block per plane finds the digit-1 bucket of each rank
 //   k_med_collect : grid pass over R appending the keys that fall in those buckets
 //   k_med_final   : one block per plane resolves digits 2 (12 bits) and 3 (8 bits)
@@ -18,7 +18,8 @@ __global__ void __launch_bounds__(256) k_med_scan(const uint32_t* __restrict__ h
   __shared__ uint32_t s_scan[256];
   __shared__ uint32_t s_out[2];
   const int b = blockIdx.x;
-  for (int i = threadIdx.x; i < kHistBins; i += 256) s_h[i] = hist[(int64_t)b * kHistBins + i];
+  for (int i = threadIdx.x; i < kHistBins; i += 256)
+    s_h[i] = i < kMedBins1 ? hist[(int64_t)b * kMedBins1 + i] : 0u;
   __syncthreads();
   uint32_t k1 = (n % 2 == 1) ? (uint32_t)(n / 2) : (uint32_t)(n / 2 - 1);
   uint32_t k2 = (uint32_t)(n / 2);
@@ -60,7 +61,7 @@ __global__ void __launch_bounds__(256) k_med_collect(const float* __restrict__ R
     keys[q] = 0;
     if (i < n) {
       uint32_t key = fkey(Rp[i]);
-      uint32_t d = key >> (32 - kHistBits);
+      uint32_t d = key >> (32 - kMedBits1);
       keys[q] = key;
       if (d == b1 || d == b2) mask |= 1u << q;
     }
@@ -73,35 +74,35 @@ __global__ void __launch_bounds__(256) k_med_collect(const float* __restrict__ R
     if (mask & (1u << q)) *lp++ = keys[q];
 }
 
-// Resolve one rank within bucket `bk` (the key's top 12 bits) from the collected list.
+// Resolve one rank within bucket `bk` (the key's top 11 bits) from the collected list.
 SFM_DEV uint32_t select_in_list(const uint32_t* lp, int64_t m, uint32_t bk, uint32_t rank,
                                 uint32_t* s_h, uint32_t* s_scan, uint32_t* s_out) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  // digit 2: bits [19:8]
+  // digit 2: bits [20:10]
   for (int i = tid; i < kHistBins; i += nt) s_h[i] = 0u;
   __syncthreads();
   for (int64_t i = tid; i < m; i += nt) {
     uint32_t k = lp[i];
-    if ((k >> 20) == bk) atomicAdd(&s_h[(k >> 8) & 0xfffu], 1u);
+    if ((k >> 21) == bk) atomicAdd(&s_h[(k >> 10) & 0x7ffu], 1u);
   }
   __syncthreads();
   find_bin(s_h, kHistBins, rank, s_scan, s_out);
   uint32_t d2 = s_out[0];
   rank -= s_out[1];
-  uint32_t pre = (bk << 12) | d2;  // top 24 bits
+  uint32_t pre = (bk << 11) | d2;  // top 22 bits
   __syncthreads();
-  // digit 3: bits [7:0] (histogram padded to 4096 bins for find_bin)
+  // digit 3: bits [9:0] (histogram padded to 4096 bins for find_bin)
   for (int i = tid; i < kHistBins; i += nt) s_h[i] = 0u;
   __syncthreads();
   for (int64_t i = tid; i < m; i += nt) {
     uint32_t k = lp[i];
-    if ((k >> 8) == pre) atomicAdd(&s_h[k & 0xffu], 1u);
+    if ((k >> 10) == pre) atomicAdd(&s_h[k & 0x3ffu], 1u);
   }
   __syncthreads();
   find_bin(s_h, kHistBins, rank, s_scan, s_out);
   uint32_t d3 = s_out[0];
   __syncthreads();
-  return (pre << 8) | d3;
+  return (pre << 10) | d3;
 }
 
 __global__ void __launch_bounds__(1024) k_med_final(MedianState* __restrict__ st,

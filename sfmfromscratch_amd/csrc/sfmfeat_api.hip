@@ -192,7 +192,7 @@ int reserve_impl(sfm_ctx* c, int B, int H, int W) {
   if ((rc = ensure(c, c->d_img0, (size_t)B * A0 * 4))) return rc;
   if ((rc = ensure(c, c->d_lvl, (size_t)B * Arest * 4))) return rc;
   if ((rc = ensure(c, c->d_R, (size_t)B * A0 * 4))) return rc;
-  if ((rc = ensure(c, c->d_hist, (size_t)c->L * B * kHistBins * 4))) return rc;
+  if ((rc = ensure(c, c->d_hist, (size_t)c->L * B * kMedBins1 * 4))) return rc;
   if ((rc = ensure(c, c->d_med, (size_t)c->L * B * sizeof(MedianState)))) return rc;
   if ((rc = ensure(c, c->d_medlist, (size_t)B * A0 * 4))) return rc;
   if ((rc = ensure(c, c->d_counts, (size_t)2 * c->L * B * 8 * kCounterStride))) return rc;
@@ -229,14 +229,14 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
       off += (int64_t)B * lv[l].h * lv[l].w;
     }
   }
-  HIPCHK(c, hipMemsetAsync(c->d_hist.p, 0, (size_t)L * B * kHistBins * 4, st));
+  HIPCHK(c, hipMemsetAsync(c->d_hist.p, 0, (size_t)L * B * kMedBins1 * 4, st));
   HIPCHK(c, hipMemsetAsync(c->d_counts.p, 0, (size_t)2 * L * B * 8 * kCounterStride, st));
   unsigned long long* medcnt = as<unsigned long long>(c->d_counts);
   unsigned long long* candcnt = medcnt + (size_t)L * B * kCounterStride;
   const float alpha = (float)c->p.alpha;  // NEP 50: the python float becomes float32
   for (int l = 0; l < L; ++l) {
     const int h = lv[l].h, w = lv[l].w;
-    uint32_t* hist = as<uint32_t>(c->d_hist) + (size_t)l * B * kHistBins;
+    uint32_t* hist = as<uint32_t>(c->d_hist) + (size_t)l * B * kMedBins1;
     MedianState* med = as<MedianState>(c->d_med) + (size_t)l * B;
     {
       StageScope sc(c, SFM_PROF_HARRIS, st);
