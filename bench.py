@@ -8,9 +8,10 @@ feature width 18), then NNRatioFeatureMatcher(0.85) over consecutive pairs — t
 reference's schedule (Runner.py:183).  One step = extract the batch + match its pairs.
 
 Multi-GPU (weak scaling, one process per GPU, torchrun): rank r owns frames
-[r*B, (r+1)*B) of one global sequence.  The only exchange is the reference's consecutive
-pair that straddles two shards: the first slot of every rank's descriptor table is
-all-gathered over RCCL and rank r also matches (its last frame, rank r+1's first frame).
+[r*B, (r+1)*B) of one global sequence (sfmfromscratch_amd/distributed.py).  The only
+exchange is the reference's consecutive pair that straddles two shards: rank r+1 sends
+its first slot (xy, desc, count) to rank r over RCCL point-to-point, and rank r also
+matches (its last frame, rank r+1's first frame).
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus `roofline`
 (dominant kernel, live HIP-event timing inside the timed region) and `cpu_baseline`
@@ -46,18 +47,39 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(sample_frames: int):
-    """The C oracle (scalar restatement, 1 thread) on `sample_frames` 1080p frames and
-    their consecutive pairs; returns images/s."""
+def cpu_threads() -> int:
+    """Host cores this process may use (the GPU box's share is 16; os.cpu_count() there
+    reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+
+
+def cpu_baseline(frames_per_thread: int):
+    """The C restatement in oracle/ (scalar code, one image per thread, ctypes releases
+    the GIL) on `threads * frames_per_thread` 1080p frames and their consecutive pairs,
+    each thread owning a contiguous block of frames; returns (images/s, seconds, threads,
+    frames)."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from oracle import oracle as O
     from sfmfromscratch_amd import synth
-    imgs = [synth.make_frame(H, W, 1234, i) for i in range(sample_frames)]
+    nt = cpu_threads()
+    n = nt * frames_per_thread
+    imgs = [synth.make_frame(H, W, 1234, i) for i in range(n)]
+
+    def block(t):
+        descs = [O.extract(imgs[i], P_OCT)[2] for i in range(t * frames_per_thread, (t + 1) * frames_per_thread)]
+        for a, b in zip(descs, descs[1:]):
+            O.match(a, b, RATIO)
+
     t0 = time.perf_counter()
-    descs = [O.extract(im, P_OCT)[2] for im in imgs]
-    for i in range(sample_frames - 1):
-        O.match(descs[i], descs[i + 1], RATIO)
+    with ThreadPoolExecutor(nt) as pool:
+        list(pool.map(block, range(nt)))
     dt = time.perf_counter() - t0
-    return sample_frames / dt, dt
+    return n / dt, dt, nt, n
 
 
 def main():
@@ -66,7 +88,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=4, help="frames in the CPU baseline sample (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=2,
+                    help="frames per host thread in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="disable the live per-stage HIP events")
     args = ap.parse_args()
 
@@ -81,8 +104,9 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    from sfmfromscratch_amd import distributed as D
     from sfmfromscratch_amd import synth
-    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, SlotTable, consecutive_pairs
+    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, SlotTable
 
     B = args.batch
     ex = BatchExtractor(P_OCT, device=local)
@@ -94,30 +118,20 @@ def main():
     frames_u8 = np.stack([synth.make_frame_u8(H, W, 1234, rank * B + i) for i in range(B)])
     frames = torch.from_numpy(synth.u8_to_gray(frames_u8)).to(dev)
     del frames_u8
-    slots = SlotTable(torch, B + 1, cap, dev)           # slot B = neighbour's first frame (halo)
-    has_next = rank < world - 1
-    pairs_np = consecutive_pairs(B)
-    if has_next:
-        pairs_np = np.concatenate([pairs_np, np.array([[B - 1, B]], np.int32)])
+    slots = SlotTable(torch, B + 1, cap, dev)           # slot B = next rank's first frame (halo)
+    pairs_np = D.local_consecutive_pairs(B, rank, world)
     pairs = torch.from_numpy(pairs_np).to(dev)
     P = pairs.shape[0]
     mout = (torch.zeros((P, cap, 2), dtype=torch.int32, device=dev),
             torch.zeros((P, cap), dtype=torch.float32, device=dev),
             torch.zeros((P,), dtype=torch.int32, device=dev))
-    gath_desc = torch.zeros((world, cap, 128), dtype=torch.float32, device=dev) if world > 1 else None
-    gath_cnt = torch.zeros((world,), dtype=torch.int32, device=dev) if world > 1 else None
 
     class View:  # the first B rows of the slot table, as the extractor's output
         xy, desc, count = slots.xy[:B], slots.desc[:B], slots.count[:B]
 
     def step():
         ex.extract(frames, out=View)
-        if world > 1:
-            dist.all_gather_into_tensor(gath_desc, slots.desc[0].contiguous())
-            dist.all_gather_into_tensor(gath_cnt, slots.count[0:1].contiguous())
-            if has_next:
-                slots.desc[B].copy_(gath_desc[rank + 1])
-                slots.count[B:B + 1].copy_(gath_cnt[rank + 1:rank + 2])
+        D.halo_exchange(dist, slots, B, rank, world)
         matcher.match(slots, pairs, out=mout)
 
     for _ in range(args.warmup):
@@ -181,10 +195,11 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        v, dt = cpu_baseline(args.cpu_sample)
-        cpu = {"value": round(v, 4), "unit": "images/sec", "cores": 1, "kind": "port",
-               "sample": f"oracle/sfm_oracle.c (C restatement, 1 thread) on {args.cpu_sample} synthetic "
-                         f"1080p frames + {args.cpu_sample - 1} consecutive pairs, {dt:.1f} s"}
+        v, dt, nt, nf = cpu_baseline(args.cpu_sample)
+        cpu = {"value": round(v, 4), "unit": "images/sec", "cores": nt, "kind": "port",
+               "sample": f"oracle/sfm_oracle.c (scalar C restatement) on {nt} host threads, each extracting "
+                         f"{args.cpu_sample} synthetic 1080p frames and matching their consecutive pair "
+                         f"({nf} frames, {nt * (args.cpu_sample - 1)} pairs) in {dt:.1f} s"}
 
     if rank == 0:
         out = {

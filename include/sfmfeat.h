@@ -193,9 +193,15 @@ int32_t sfm_debug_harris(int32_t device, const float* gauss, int32_t gs, double 
                          float* median_out, int64_t* ncand_out);
 
 /* Mean time (ms) of one fused Harris launch on synthetic planes, ablation variant abl
- * (0 full, 1 no digit histogram, 2 no window sums, 3 no Sobel/products). */
+ * (0 full, 1 no digit histogram, 2 no window sums, 3 no Sobel/products, 4 image load +
+ * R store only, 5 R store only). */
 float sfm_debug_time_harris(int32_t device, int32_t abl, int32_t B, int32_t H, int32_t W,
                             int32_t iters);
+
+/* Keypoint selection of the context's last extraction (synchronises the device): planes
+ * (image x level) that took the exact-median path, and planes in total.  The default
+ * certified select decides the others from the Harris histogram alone. */
+int32_t sfm_debug_select_stats(sfm_ctx* ctx, int32_t* fallback_planes, int32_t* total_planes);
 
 #ifdef __cplusplus
 }

@@ -50,6 +50,7 @@ SIGNATURES = {
     "sfm_profile_enable": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "sfm_profile_read": (ctypes.c_int32, [_vp, ctypes.POINTER(ctypes.c_double), _i64p, ctypes.c_int32]),
     "sfm_debug_time_harris": (ctypes.c_float, [ctypes.c_int32] * 6),
+    "sfm_debug_select_stats": (ctypes.c_int32, [_vp, _i32p, _i32p]),
     "sfm_debug_atan2": (ctypes.c_int32, [ctypes.c_int32, _fp, _fp, _fp, ctypes.c_int64]),
     "sfm_debug_harris": (ctypes.c_int32, [ctypes.c_int32, _fp, ctypes.c_int32, ctypes.c_double, ctypes.c_int32,
                                           _fp, ctypes.c_int32, ctypes.c_int32, _fp, _fp, _i64p]),
@@ -154,6 +155,12 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def select_stats(self):
+        """(planes that took the exact-median path, planes) of the last extraction."""
+        fb, tot = ctypes.c_int32(0), ctypes.c_int32(0)
+        check(self.lib.sfm_debug_select_stats(self.handle, ctypes.byref(fb), ctypes.byref(tot)), self.handle)
+        return int(fb.value), int(tot.value)
 
     # -------- host-pointer API (drop-in path) --------
     def extract(self, img: np.ndarray):

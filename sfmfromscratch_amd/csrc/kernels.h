@@ -22,12 +22,24 @@ constexpr int kTopkLdsCap = 8192;           // max keys sorted in LDS by the top
 constexpr int kMaxMatchRows = 16384;        // max keypoints per image for the matcher sort
 constexpr int kCounterStride = 32;          // u64 per per-plane atomic counter (own 256-B line)
 
-// Per-plane state of the exact median (np.median, NaiveSIFT.py:91).
+// Per-plane state of the keypoint selection (NaiveSIFT.py:90-120).
+//
+// Certified select (default): the reference keeps R == window max && R >= median, then the
+// k largest.  NMS collects the window maxima with key >= tnms (a volume threshold: about
+// vmin pixels lie above it).  If at least k were found and the k-th largest has key >=
+// tcert (the first key above the median's digit-1 bucket), all of the top k are >= the
+// median and every reference candidate outranking the k-th was found: the top k equal
+// the reference's whatever the exact median is — so the median is only bounded, from the
+// Harris histogram.  Other planes (and forced exact mode) set `fallback` and run the
+// exact path: np.median by radix select, then the full NMS predicate.
 struct MedianState {
-  uint32_t bucket[2];   // top-12-bit digit holding rank k1 / k2
+  uint32_t bucket[2];   // digit-1 (top 11 bits) bucket holding rank k1 / k2
   uint32_t rank[2];     // residual rank inside that bucket
   uint32_t odd;         // H*W odd -> median is element k1 alone
-  float median;         // result
+  float median;         // exact median (fallback planes only)
+  uint32_t tnms;        // certified select: candidate threshold key
+  uint32_t tcert;       // certified select: the k-th key must reach this
+  uint32_t fallback;    // 1: this plane takes the exact path
 };
 
 // Per-plane keypoint list produced by the top-k kernel (level coordinates).
@@ -50,22 +62,29 @@ void launch_harris(const float* lvl, float* R, uint32_t* hist, int B, int H, int
 float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
                            const float* gk, float alpha, int iters);
 
-// median.hip
-void launch_median(const float* R, uint32_t* hist, MedianState* state, uint32_t* list,
-                   unsigned long long* list_count, int B, int H, int W, hipStream_t st);
+// median.hip.  launch_select_scan: median buckets + certified threshold per plane
+// (vmin = pixels required at or above the threshold).  launch_median_exact: the exact
+// median of the planes flagged `fallback`.
+void launch_select_scan(const uint32_t* hist, MedianState* state, unsigned long long* list_count, int B,
+                        int H, int W, int64_t vmin, int force_exact, hipStream_t st);
+void launch_median_exact(const float* R, MedianState* state, uint32_t* list, unsigned long long* list_count,
+                         int B, int H, int W, hipStream_t st);
 
-// nms.hip: candidates (R == window max, or R == 0 below the median) as 64-bit keys
-// (~fkey(conf) << 32 | raster index), appended per plane.
+// nms.hip: candidates as 64-bit keys (~fkey(conf) << 32 | raster index), appended per
+// plane.  mode 0 (certified planes): R == window max && key(R) >= tnms; mode 1 (fallback
+// planes): the exact predicate (R == window max, or R == 0 below the median).
 void launch_nms(const float* R, const MedianState* state, uint64_t* cand,
-                unsigned long long* cand_count, int B, int H, int W, int ksize, hipStream_t st);
+                unsigned long long* cand_count, int B, int H, int W, int ksize, int mode, hipStream_t st);
 
 // select.hip: top-k by (conf desc, index asc) + edge filter (NaiveSIFT.py:99-120).
 void init_topk_attributes();
 void init_describe_attributes(size_t max_lds);
 size_t describe_lds_bytes(int fw, int rotate);
+// mode 0: certified planes (a plane with fewer than k candidates is flagged fallback and
+// left unwritten); mode 1: fallback planes only.
 void launch_topk(const uint64_t* cand, const unsigned long long* cand_count, uint64_t* scratch,
                  KpList kp, int kcap, int k, int B, int H, int W, int half_window,
-                 hipStream_t st);
+                 MedianState* state, int mode, hipStream_t st);
 
 // describe.hip: descriptors of one level written into the output slot table.
 void launch_describe(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp,

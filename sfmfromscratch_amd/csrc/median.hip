@@ -3,17 +3,24 @@
 //   even H*W: float32 (v[k1] + v[k2]) / 2 with k1 = n/2-1, k2 = n/2
 //   odd  H*W: v[n/2]
 // Digit 1 (top 11 bits) is histogrammed inside the Harris kernel.  Then:
-//   k_med_scan    : one block per plane finds the digit-1 bucket of each rank
+//   k_med_scan    : one block per plane finds the digit-1 bucket of each rank and the
+//                   certified-select threshold (kernels.h, MedianState)
 //   k_med_collect : grid pass over R appending the keys that fall in those buckets
-//   k_med_final   : one block per plane resolves digits 2 (12 bits) and 3 (8 bits)
+//   k_med_final   : one block per plane resolves digits 2 (11 bits) and 3 (10 bits)
+// collect / final run only for planes flagged `fallback` (the exact path).
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace sfm {
 
+// Buckets from 2^126 up (and inf / NaN) never certify: (lo + hi) / 2 could overflow.
+constexpr uint32_t kHugeBucket = 0x7F4u;
+
 __global__ void __launch_bounds__(256) k_med_scan(const uint32_t* __restrict__ hist,
                                                   MedianState* __restrict__ st,
                                                   unsigned long long* __restrict__ list_count,
-                                                  int64_t n) {
+                                                  int64_t n, int64_t vmin, int force_exact) {
   __shared__ uint32_t s_h[kHistBins];
   __shared__ uint32_t s_scan[256];
   __shared__ uint32_t s_out[2];
@@ -28,7 +35,20 @@ __global__ void __launch_bounds__(256) k_med_scan(const uint32_t* __restrict__ h
   __syncthreads();
   find_bin(s_h, kHistBins, k2, s_scan, s_out);
   uint32_t b2 = s_out[0], r2 = k2 - s_out[1];
+  __syncthreads();
+  // candidate threshold: the bucket holding the vmin-th largest value (so >= vmin values
+  // lie at or above it), at least the median's lower bucket b1 (nothing below certifies)
+  uint32_t tb = 0;
+  if (n > vmin) {
+    find_bin(s_h, kHistBins, (uint32_t)(n - vmin), s_scan, s_out);
+    tb = s_out[0];
+  }
+  tb = max(tb, b1);
+  const bool certifiable = !force_exact && b2 < kHugeBucket;
   if (threadIdx.x == 0) {
+    st[b].tnms = tb << (32 - kMedBits1);
+    st[b].tcert = certifiable ? (b2 + 1) << (32 - kMedBits1) : 0xffffffffu;
+    st[b].fallback = certifiable ? 0u : 1u;
     st[b].bucket[0] = b1;
     st[b].bucket[1] = b2;
     st[b].rank[0] = r1;
@@ -39,9 +59,10 @@ __global__ void __launch_bounds__(256) k_med_scan(const uint32_t* __restrict__ h
 }
 
 constexpr int kCollectPerThread = 16;
+constexpr int kCollectBlocksPerPlane = 64;
 
-// Each workgroup scans 256 * 16 consecutive keys and appends the ones in the two target
-// buckets with one global atomic (block_append).
+// Each workgroup scans chunks of 256 * 16 consecutive keys and appends the ones in the two
+// target buckets with one global atomic per chunk (block_append).  Certified planes exit.
 __global__ void __launch_bounds__(256) k_med_collect(const float* __restrict__ R,
                                                      const MedianState* __restrict__ st,
                                                      uint32_t* __restrict__ list,
@@ -50,28 +71,32 @@ __global__ void __launch_bounds__(256) k_med_collect(const float* __restrict__ R
   __shared__ uint32_t s_wsum[4];
   __shared__ unsigned long long s_base;
   const int b = blockIdx.y;
+  if (!st[b].fallback) return;
   const uint32_t b1 = st[b].bucket[0], b2 = st[b].bucket[1];
   const float* Rp = R + (int64_t)b * n;
-  const int64_t base = (int64_t)blockIdx.x * 256 * kCollectPerThread;
-  uint32_t keys[kCollectPerThread];
-  uint32_t mask = 0;
+  const int64_t nchunks = (n + 256 * kCollectPerThread - 1) / (256 * kCollectPerThread);
+  for (int64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    const int64_t base = chunk * 256 * kCollectPerThread;
+    uint32_t keys[kCollectPerThread];
+    uint32_t mask = 0;
 #pragma unroll
-  for (int q = 0; q < kCollectPerThread; ++q) {
-    int64_t i = base + (int64_t)q * 256 + threadIdx.x;  // coalesced
-    keys[q] = 0;
-    if (i < n) {
-      uint32_t key = fkey(Rp[i]);
-      uint32_t d = key >> (32 - kMedBits1);
-      keys[q] = key;
-      if (d == b1 || d == b2) mask |= 1u << q;
+    for (int q = 0; q < kCollectPerThread; ++q) {
+      int64_t i = base + (int64_t)q * 256 + threadIdx.x;  // coalesced
+      keys[q] = 0;
+      if (i < n) {
+        uint32_t key = fkey(Rp[i]);
+        uint32_t d = key >> (32 - kMedBits1);
+        keys[q] = key;
+        if (d == b1 || d == b2) mask |= 1u << q;
+      }
     }
-  }
-  int64_t slot = block_append(&list_count[(int64_t)b * kCounterStride], (uint32_t)__popc(mask), s_wsum,
-                              &s_base);
-  uint32_t* lp = list + (int64_t)b * n + slot;
+    int64_t slot = block_append(&list_count[(int64_t)b * kCounterStride], (uint32_t)__popc(mask), s_wsum,
+                                &s_base);
+    uint32_t* lp = list + (int64_t)b * n + slot;
 #pragma unroll
-  for (int q = 0; q < kCollectPerThread; ++q)
-    if (mask & (1u << q)) *lp++ = keys[q];
+    for (int q = 0; q < kCollectPerThread; ++q)
+      if (mask & (1u << q)) *lp++ = keys[q];
+  }
 }
 
 // Resolve one rank within bucket `bk` (the key's top 11 bits) from the collected list.
@@ -113,6 +138,7 @@ __global__ void __launch_bounds__(1024) k_med_final(MedianState* __restrict__ st
   __shared__ uint32_t s_scan[1024];
   __shared__ uint32_t s_out[2];
   const int b = blockIdx.x;
+  if (!st[b].fallback) return;
   const uint32_t* lp = list + (int64_t)b * n;
   const int64_t m = (int64_t)list_count[(int64_t)b * kCounterStride];
   MedianState s = st[b];
@@ -130,11 +156,17 @@ __global__ void __launch_bounds__(1024) k_med_final(MedianState* __restrict__ st
   if (threadIdx.x == 0) st[b].median = med;
 }
 
-void launch_median(const float* R, uint32_t* hist, MedianState* state, uint32_t* list,
-                   unsigned long long* list_count, int B, int H, int W, hipStream_t st) {
+void launch_select_scan(const uint32_t* hist, MedianState* state, unsigned long long* list_count, int B,
+                        int H, int W, int64_t vmin, int force_exact, hipStream_t st) {
   int64_t n = (int64_t)H * W;
-  hipLaunchKernelGGL(k_med_scan, dim3(B), dim3(256), 0, st, hist, state, list_count, n);
-  int gx = (int)((n + 256 * kCollectPerThread - 1) / (256 * kCollectPerThread));
+  hipLaunchKernelGGL(k_med_scan, dim3(B), dim3(256), 0, st, hist, state, list_count, n, vmin, force_exact);
+}
+
+void launch_median_exact(const float* R, MedianState* state, uint32_t* list, unsigned long long* list_count,
+                         int B, int H, int W, hipStream_t st) {
+  int64_t n = (int64_t)H * W;
+  int64_t nchunks = (n + 256 * kCollectPerThread - 1) / (256 * kCollectPerThread);
+  int gx = (int)std::min<int64_t>(nchunks, kCollectBlocksPerPlane);
   hipLaunchKernelGGL(k_med_collect, dim3(gx, B), dim3(256), 0, st, R, state, list, list_count, n);
   hipLaunchKernelGGL(k_med_final, dim3(B), dim3(1024), 0, st, state, list, list_count, n);
 }

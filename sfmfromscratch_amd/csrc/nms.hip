@@ -1,5 +1,4 @@
-// nms.hip — max-pool NMS + median threshold + candidate compaction
-// (NaiveSIFT.py:77-97):
+// nms.hip — max-pool NMS + threshold + candidate compaction (NaiveSIFT.py:77-97):
 //   R_maxpool[r,c] = max of R over the ksize x ksize window clipped to the image (:85-88)
 //   R_maxpool[R < median] = 0                                                    (:92)
 //   candidate  <=> R == R_maxpool                                                (:95)
@@ -7,93 +6,228 @@
 // per plane as 64-bit keys ~fkey(R) << 32 | raster index, so ascending key order is the
 // reference's confidence-descending order with ties broken by raster index.
 //
-// Max is exact, so the window max is computed separably (row max, then column max) on an
-// LDS tile; out-of-image cells hold -inf and never win (the window is clipped).
+// Two predicates (kernels.h, MedianState):
+//   mode 0 (certified planes): key(R) >= tnms && R == window max — a few percent of the
+//          pixels pass the threshold, and only those test their window;
+//   mode 1 (fallback planes):  the exact predicate above with the exact median.
+// "R == window max" is tested as "no cell of the clipped window is larger"; out-of-image
+// cells hold -inf and never win.
+//
+// k_nms_tile (ksize <= 9): persistent workgroups walk 64 x 32 tiles of one plane; the tile
+// + halo (72-float rows, 16-B aligned) is loaded with 16-B loads into registers one tile
+// ahead, then staged through LDS.  HBM-bound: ~1.2 reads of R.
+// k_nms_generic (larger ksize): separable window max on an LDS tile.
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace sfm {
 
 constexpr int kNT_W = 64;
 constexpr int kNT_H = 32;
-constexpr int kRowsPerThread = kNT_H / 4;  // 256 threads = 64 columns x 4 row groups
+constexpr int kNmsBlocksPerPlane = 64;
 
-template <int KH>  // KH = ksize // 2 (KH_MAX = SFM_NMS_MAX_HALF when instantiated generic)
-__global__ void __launch_bounds__(256) k_nms(const float* __restrict__ R,
-                                             const MedianState* __restrict__ st,
-                                             uint64_t* __restrict__ cand,
-                                             unsigned long long* __restrict__ cand_count, int H,
-                                             int W, int kh, int tiles_x) {
-  constexpr int KM = KH;  // LDS sized for the template half-width
-  __shared__ float s_r[kNT_H + 2 * KM][kNT_W + 2 * KM];
-  __shared__ float s_m[kNT_H + 2 * KM][kNT_W];
+template <int KH, int MODE>
+__global__ void __launch_bounds__(256) k_nms_tile(const float* __restrict__ R,
+                                                  const MedianState* __restrict__ st,
+                                                  uint64_t* __restrict__ cand,
+                                                  unsigned long long* __restrict__ cand_count, int H,
+                                                  int W, int tiles_x, int ntiles) {
+  static_assert(KH <= 4, "72-float rows hold a 4-column halo");
+  constexpr int LW = 72;                // tile columns tx0-4 .. tx0+67
+  constexpr int LW4 = LW / 4;
+  constexpr int LH = kNT_H + 2 * KH;
+  constexpr int NV4 = LH * LW4;
+  constexpr int PER = (NV4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float s_t[LH][LW];
   __shared__ uint32_t s_wsum[4];
   __shared__ unsigned long long s_base;
   const int tid = threadIdx.x;
   const int b = blockIdx.y;
-  const int tx0 = (blockIdx.x % tiles_x) * kNT_W;
-  const int ty0 = (blockIdx.x / tiles_x) * kNT_H;
+  const bool fb = st[b].fallback != 0;
+  if (MODE == 0 ? fb : !fb) return;
+  const uint32_t tnms = st[b].tnms;
+  const float med = st[b].median;
   const int64_t n = (int64_t)H * W;
   const float* Rp = R + (int64_t)b * n;
-  const int TWh = kNT_W + 2 * kh, THh = kNT_H + 2 * kh;
-  for (int idx = tid; idx < THh * TWh; idx += 256) {
-    int iy = idx / TWh, ix = idx - iy * TWh;
-    int gy = ty0 - kh + iy, gx = tx0 - kh + ix;
-    float v = -INFINITY;  // outside the image: never the (clipped) window max
-    if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = Rp[(int64_t)gy * W + gx];
-    s_r[iy][ix] = v;
-  }
-  __syncthreads();
-  for (int idx = tid; idx < THh * kNT_W; idx += 256) {
-    int iy = idx / kNT_W, ix = idx - iy * kNT_W;
-    float m = s_r[iy][ix];
-    for (int d = 1; d <= 2 * kh; ++d) m = fmaxf(m, s_r[iy][ix + d]);
-    s_m[iy][ix] = m;
-  }
-  __syncthreads();
-  const float med = st[b].median;
-  const int c = tid & 63;
-  const int rg = tid >> 6;
-  uint32_t flags = 0;
+  const bool vec = (W & 3) == 0;  // 16-B aligned rows (the plane base too: n % 4 == 0)
+
+  float4 t[PER];
+  auto prefetch = [&](int tile) {
+    const int x0 = (tile % tiles_x) * kNT_W - 4;
+    const int y0 = (tile / tiles_x) * kNT_H - KH;
 #pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q) {
-    const int r = rg * kRowsPerThread + q;
-    const int gy = ty0 + r, gx = tx0 + c;
-    if (gy < H && gx < W) {
-      float m = s_m[r][c];
-      for (int d = 1; d <= 2 * kh; ++d) m = fmaxf(m, s_m[r + d][c]);
-      const float v = s_r[r + kh][c + kh];
-      const bool pred = (v < med) ? (v == 0.0f) : (v == m);
+    for (int k = 0; k < PER; ++k) {
+      const int e = tid + 256 * k;
+      const int row = e / LW4, c4 = e - row * LW4;
+      const int gy = y0 + row, gx = x0 + 4 * c4;
+      const bool rowok = e < NV4 && gy >= 0 && gy < H;
+      const int yc = min(max(gy, 0), H - 1);
+      if (vec) {
+        const int xc = min(max(gx, 0), W - 4);
+        const float4 v = *reinterpret_cast<const float4*>(Rp + (int64_t)yc * W + xc);
+        const bool ok = rowok && gx >= 0 && gx < W;  // W % 4 == 0: a float4 is all in or all out
+        t[k] = ok ? v : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      } else {
+        float q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int x = gx + j;
+          const float v = Rp[(int64_t)yc * W + min(max(x, 0), W - 1)];
+          q[j] = (rowok && x >= 0 && x < W) ? v : -INFINITY;
+        }
+        t[k] = make_float4(q[0], q[1], q[2], q[3]);
+      }
+    }
+  };
+
+  const int r = tid >> 3;          // output row in the tile
+  const int c0 = (tid & 7) * 8;    // 8 output columns
+  if (blockIdx.x < ntiles) prefetch(blockIdx.x);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int tx0 = (tile % tiles_x) * kNT_W;
+    const int ty0 = (tile / tiles_x) * kNT_H;
+    __syncthreads();  // previous tile's LDS reads done
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = tid + 256 * k;
+      if (e < NV4) reinterpret_cast<float4*>(&s_t[0][0])[e] = t[k];
+    }
+    __syncthreads();
+    if (tile + (int)gridDim.x < ntiles) prefetch(tile + gridDim.x);
+    uint32_t flags = 0;
+    float vals[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int c = c0 + q;
+      const float v = s_t[r + KH][4 + c];
+      vals[q] = v;
+      const bool inside = ty0 + r < H && tx0 + c < W;
+      bool pred = false;
+      if (inside && (MODE == 1 || fkey(v) >= tnms)) {
+        if (MODE == 1 && v < med) {
+          pred = (v == 0.0f);  // R_maxpool[R < median] = 0 (:92)
+        } else {
+          bool ismax = true;
+#pragma unroll
+          for (int dy = -KH; dy <= KH; ++dy)
+#pragma unroll
+            for (int dx = -KH; dx <= KH; ++dx) ismax &= !(s_t[r + KH + dy][4 + c + dx] > v);
+          pred = ismax;
+        }
+      }
       flags |= pred ? (1u << q) : 0u;
     }
-  }
-  const int64_t slot = block_append(&cand_count[(int64_t)b * kCounterStride], (uint32_t)__popc(flags), s_wsum,
-                                    &s_base);
-  uint64_t* out = cand + (int64_t)b * n + slot;
+    if (__syncthreads_or(flags != 0)) {
+      const int64_t slot = block_append(&cand_count[(int64_t)b * kCounterStride], (uint32_t)__popc(flags),
+                                        s_wsum, &s_base);
+      uint64_t* out = cand + (int64_t)b * n + slot;
 #pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q) {
-    if (flags & (1u << q)) {
-      const int r = rg * kRowsPerThread + q;
-      const int gy = ty0 + r, gx = tx0 + c;
-      const float v = s_r[r + kh][c + kh];
-      *out++ = ((uint64_t)(~fkey(v)) << 32) | (uint32_t)(gy * W + gx);
+      for (int q = 0; q < 8; ++q)
+        if (flags & (1u << q))
+          *out++ = ((uint64_t)(~fkey(vals[q])) << 32) | (uint32_t)((ty0 + r) * W + tx0 + c0 + q);
     }
   }
 }
 
+constexpr int kRowsPerThread = kNT_H / 4;  // 256 threads = 64 columns x 4 row groups
+
+template <int KH>  // LDS sized for half-width KH (SFM_NMS_MAX_HALF); kh <= KH at run time
+__global__ void __launch_bounds__(256) k_nms_generic(const float* __restrict__ R,
+                                                     const MedianState* __restrict__ st,
+                                                     uint64_t* __restrict__ cand,
+                                                     unsigned long long* __restrict__ cand_count, int H,
+                                                     int W, int kh, int tiles_x, int ntiles, int mode) {
+  __shared__ float s_r[kNT_H + 2 * KH][kNT_W + 2 * KH];
+  __shared__ float s_m[kNT_H + 2 * KH][kNT_W];
+  __shared__ uint32_t s_wsum[4];
+  __shared__ unsigned long long s_base;
+  const int tid = threadIdx.x;
+  const int b = blockIdx.y;
+  const bool fb = st[b].fallback != 0;
+  if (mode == 0 ? fb : !fb) return;
+  const uint32_t tnms = st[b].tnms;
+  const float med = st[b].median;
+  const int64_t n = (int64_t)H * W;
+  const float* Rp = R + (int64_t)b * n;
+  const int TWh = kNT_W + 2 * kh, THh = kNT_H + 2 * kh;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int tx0 = (tile % tiles_x) * kNT_W;
+    const int ty0 = (tile / tiles_x) * kNT_H;
+    __syncthreads();
+    for (int idx = tid; idx < THh * TWh; idx += 256) {
+      int iy = idx / TWh, ix = idx - iy * TWh;
+      int gy = ty0 - kh + iy, gx = tx0 - kh + ix;
+      float v = -INFINITY;  // outside the image: never the (clipped) window max
+      if (gy >= 0 && gy < H && gx >= 0 && gx < W) v = Rp[(int64_t)gy * W + gx];
+      s_r[iy][ix] = v;
+    }
+    __syncthreads();
+    for (int idx = tid; idx < THh * kNT_W; idx += 256) {
+      int iy = idx / kNT_W, ix = idx - iy * kNT_W;
+      float m = s_r[iy][ix];
+      for (int d = 1; d <= 2 * kh; ++d) m = fmaxf(m, s_r[iy][ix + d]);
+      s_m[iy][ix] = m;
+    }
+    __syncthreads();
+    const int c = tid & 63;
+    const int rg = tid >> 6;
+    uint32_t flags = 0;
+#pragma unroll
+    for (int q = 0; q < kRowsPerThread; ++q) {
+      const int r = rg * kRowsPerThread + q;
+      const int gy = ty0 + r, gx = tx0 + c;
+      if (gy < H && gx < W) {
+        float m = s_m[r][c];
+        for (int d = 1; d <= 2 * kh; ++d) m = fmaxf(m, s_m[r + d][c]);
+        const float v = s_r[r + kh][c + kh];
+        const bool pred = mode == 0 ? (fkey(v) >= tnms && v == m) : ((v < med) ? (v == 0.0f) : (v == m));
+        flags |= pred ? (1u << q) : 0u;
+      }
+    }
+    const int64_t slot = block_append(&cand_count[(int64_t)b * kCounterStride], (uint32_t)__popc(flags),
+                                      s_wsum, &s_base);
+    uint64_t* out = cand + (int64_t)b * n + slot;
+#pragma unroll
+    for (int q = 0; q < kRowsPerThread; ++q) {
+      if (flags & (1u << q)) {
+        const int r = rg * kRowsPerThread + q;
+        const int gy = ty0 + r, gx = tx0 + c;
+        const float v = s_r[r + kh][c + kh];
+        *out++ = ((uint64_t)(~fkey(v)) << 32) | (uint32_t)(gy * W + gx);
+      }
+    }
+  }
+}
+
+template <int KH>
+static void launch_tile(const float* R, const MedianState* state, uint64_t* cand, unsigned long long* cnt,
+                        int B, int H, int W, int tiles_x, int ntiles, int mode, hipStream_t st) {
+  dim3 grid(std::min(ntiles, kNmsBlocksPerPlane), B);
+  if (mode == 0)
+    hipLaunchKernelGGL((k_nms_tile<KH, 0>), grid, dim3(256), 0, st, R, state, cand, cnt, H, W, tiles_x, ntiles);
+  else
+    hipLaunchKernelGGL((k_nms_tile<KH, 1>), grid, dim3(256), 0, st, R, state, cand, cnt, H, W, tiles_x, ntiles);
+}
+
 void launch_nms(const float* R, const MedianState* state, uint64_t* cand,
-                unsigned long long* cand_count, int B, int H, int W, int ksize, hipStream_t st) {
-  int kh = ksize / 2;
-  int tiles_x = (W + kNT_W - 1) / kNT_W;
-  int tiles_y = (H + kNT_H - 1) / kNT_H;
-  dim3 grid(tiles_x * tiles_y, B);
+                unsigned long long* cand_count, int B, int H, int W, int ksize, int mode, hipStream_t st) {
+  const int kh = ksize / 2;
+  const int tiles_x = (W + kNT_W - 1) / kNT_W;
+  const int tiles_y = (H + kNT_H - 1) / kNT_H;
+  const int ntiles = tiles_x * tiles_y;
   switch (kh) {
-    case 0: hipLaunchKernelGGL(k_nms<0>, grid, dim3(256), 0, st, R, state, cand, cand_count, H, W, kh, tiles_x); break;
-    case 1: hipLaunchKernelGGL(k_nms<1>, grid, dim3(256), 0, st, R, state, cand, cand_count, H, W, kh, tiles_x); break;
-    case 2: hipLaunchKernelGGL(k_nms<2>, grid, dim3(256), 0, st, R, state, cand, cand_count, H, W, kh, tiles_x); break;
-    case 3: hipLaunchKernelGGL(k_nms<3>, grid, dim3(256), 0, st, R, state, cand, cand_count, H, W, kh, tiles_x); break;
-    default:
-      hipLaunchKernelGGL(k_nms<SFM_NMS_MAX_HALF>, grid, dim3(256), 0, st, R, state, cand, cand_count, H, W, kh, tiles_x);
+    case 0: launch_tile<0>(R, state, cand, cand_count, B, H, W, tiles_x, ntiles, mode, st); break;
+    case 1: launch_tile<1>(R, state, cand, cand_count, B, H, W, tiles_x, ntiles, mode, st); break;
+    case 2: launch_tile<2>(R, state, cand, cand_count, B, H, W, tiles_x, ntiles, mode, st); break;
+    case 3: launch_tile<3>(R, state, cand, cand_count, B, H, W, tiles_x, ntiles, mode, st); break;
+    case 4: launch_tile<4>(R, state, cand, cand_count, B, H, W, tiles_x, ntiles, mode, st); break;
+    default: {
+      dim3 grid(std::min(ntiles, kNmsBlocksPerPlane), B);
+      hipLaunchKernelGGL(k_nms_generic<SFM_NMS_MAX_HALF>, grid, dim3(256), 0, st, R, state, cand, cand_count, H, W,
+                         kh, tiles_x, ntiles, mode);
       break;
+    }
   }
 }
 

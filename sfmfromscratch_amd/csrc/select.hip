@@ -2,15 +2,20 @@
 //   sort_filter = argsort(conf)[::-1][:k]   -> k smallest 64-bit candidate keys
 //   edge filter h <= y < H-h, h <= x < W-h  (h = feature_width // 2), applied AFTER top-k
 //   re-sort descending                      -> keys stay in ascending key order
-// One 1024-thread workgroup per plane.  Up to kTopkLdsCap candidates are sorted directly
+// One 1024-thread workgroup per plane.  Up to kTopkDirect candidates are sorted directly
 // in LDS; beyond that a block radix select on the confidence half of the key finds the
 // k-th key (ties on confidence resolved by raster index, exactly), and only the
 // selected k keys are sorted.
+//
+// mode 0 (certified select, kernels.h MedianState): a plane is final when it has at least
+// k candidates and the k-th key reaches tcert; otherwise it is flagged `fallback` and left
+// to mode 1, which runs after the exact median + NMS on the flagged planes only.
 #include "kernels.h"
 
 namespace sfm {
 
 constexpr int kTieLdsCap = 4096;
+constexpr int kTopkDirect = 2048;  // candidates sorted whole; above: radix select first
 
 // Block radix select over a global array of 64-bit keys on one 32-bit half.
 // use_lo = false: value = key >> 32 over all keys.  use_lo = true: value = key & ~0u over
@@ -52,7 +57,8 @@ SFM_DEV uint32_t radix_select_u32(const uint64_t* arr, int64_t m, bool use_lo, u
 __global__ void __launch_bounds__(1024) k_topk(const uint64_t* __restrict__ cand,
                                                const unsigned long long* __restrict__ cand_count,
                                                uint64_t* __restrict__ scratch, KpList kp, int kcap,
-                                               int k, int H, int W, int hw) {
+                                               int k, int H, int W, int hw,
+                                               MedianState* __restrict__ state, int mode) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
   uint64_t* s_sel = reinterpret_cast<uint64_t*>(s_raw);               // kTopkLdsCap
   uint64_t* s_tie = s_sel + kTopkLdsCap;                               // kTieLdsCap
@@ -66,13 +72,22 @@ __global__ void __launch_bounds__(1024) k_topk(const uint64_t* __restrict__ cand
   const int64_t n = (int64_t)H * W;
   const uint64_t* cp = cand + (int64_t)b * n;
   const int64_t C = (int64_t)cand_count[(int64_t)b * kCounterStride];
+  if (mode == 0) {
+    if (state[b].fallback) return;
+    if (C < (int64_t)k) {  // cannot certify: the exact path decides this plane
+      if (tid == 0) state[b].fallback = 1u;
+      return;
+    }
+  } else if (!state[b].fallback) {
+    return;
+  }
   const int kk = (int)((int64_t)k < C ? (int64_t)k : C);
   if (kk <= 0) {
     if (tid == 0) kp.count[b] = 0;
     return;
   }
   int nsel;
-  if (C <= kTopkLdsCap) {
+  if (C <= kTopkDirect) {
     const int P = next_pow2((int)C);
     for (int i = tid; i < P; i += nt) s_sel[i] = (i < C) ? cp[i] : ~0ull;
     __syncthreads();
@@ -122,6 +137,11 @@ __global__ void __launch_bounds__(1024) k_topk(const uint64_t* __restrict__ cand
     __syncthreads();
     bitonic_sort_u64(s_sel, P);
   }
+  __syncthreads();
+  if (mode == 0 && kk > 0 && ~(uint32_t)(s_sel[kk - 1] >> 32) < state[b].tcert) {
+    if (tid == 0) state[b].fallback = 1u;  // k-th candidate not above the median's bucket
+    return;
+  }
   // edge filter with order-preserving compaction
   const int per = (nsel + nt - 1) / nt;
   const int beg = tid * per;
@@ -154,9 +174,9 @@ size_t topk_lds_bytes() {
 
 void launch_topk(const uint64_t* cand, const unsigned long long* cand_count, uint64_t* scratch,
                  KpList kp, int kcap, int k, int B, int H, int W, int half_window,
-                 hipStream_t st) {
+                 MedianState* state, int mode, hipStream_t st) {
   hipLaunchKernelGGL(k_topk, dim3(B), dim3(1024), topk_lds_bytes(), st, cand, cand_count, scratch, kp,
-                     kcap, k, H, W, half_window);
+                     kcap, k, H, W, half_window, state, mode);
 }
 
 void init_topk_attributes() {

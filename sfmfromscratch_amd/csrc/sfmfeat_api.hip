@@ -50,6 +50,8 @@ struct sfm_ctx {
   DevBuf m_desc, m_count, m_pairs, m_descT, m_rows, m_matches, m_conf, m_nmatch;
   DevBuf m_hi, m_lo, m_norm2, m_rnorm, m_imgmax;
   bool match_direct = false;  // SFMFEAT_MATCH_DIRECT=1: all-pairs exact VALU kernel (A/B checks)
+  bool exact_select = false;  // SFMFEAT_SELECT=exact: every plane takes the exact-median path
+  int last_B = 0;             // planes per level of the last extraction
   // stage profiling (sfm_profile_*): HIP events bracketing each stage's launches
   bool prof = false;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
@@ -195,7 +197,7 @@ int reserve_impl(sfm_ctx* c, int B, int H, int W) {
   if ((rc = ensure(c, c->d_hist, (size_t)c->L * B * kMedBins1 * 4))) return rc;
   if ((rc = ensure(c, c->d_med, (size_t)c->L * B * sizeof(MedianState)))) return rc;
   if ((rc = ensure(c, c->d_medlist, (size_t)B * A0 * 4))) return rc;
-  if ((rc = ensure(c, c->d_counts, (size_t)2 * c->L * B * 8 * kCounterStride))) return rc;
+  if ((rc = ensure(c, c->d_counts, (size_t)3 * c->L * B * 8 * kCounterStride))) return rc;
   if ((rc = ensure(c, c->d_cand, (size_t)B * A0 * 8))) return rc;
   if ((rc = ensure(c, c->d_scratch, (size_t)B * A0 * 8))) return rc;
   size_t nk = (size_t)c->L * B * (size_t)std::max(c->kcap, 1);
@@ -216,6 +218,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   int rc = reserve_impl(c, B, H, W);
   if (rc) return rc;
   const int L = c->L;
+  c->last_B = B;
   // pyramid
   std::vector<const float*> lvl(L);
   lvl[0] = imgs;
@@ -230,38 +233,57 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     }
   }
   HIPCHK(c, hipMemsetAsync(c->d_hist.p, 0, (size_t)L * B * kMedBins1 * 4, st));
-  HIPCHK(c, hipMemsetAsync(c->d_counts.p, 0, (size_t)2 * L * B * 8 * kCounterStride, st));
+  HIPCHK(c, hipMemsetAsync(c->d_counts.p, 0, (size_t)3 * L * B * 8 * kCounterStride, st));
   unsigned long long* medcnt = as<unsigned long long>(c->d_counts);
-  unsigned long long* candcnt = medcnt + (size_t)L * B * kCounterStride;
+  unsigned long long* candcnt = medcnt + (size_t)L * B * kCounterStride;    // certified NMS
+  unsigned long long* candcnt2 = candcnt + (size_t)L * B * kCounterStride;  // fallback NMS
   const float alpha = (float)c->p.alpha;  // NEP 50: the python float becomes float32
+  // certified select: at least max(65536, 128 k) pixels at or above the threshold
+  const int64_t vmin = std::max<int64_t>(65536, (int64_t)128 * c->kcap);
   for (int l = 0; l < L; ++l) {
     const int h = lv[l].h, w = lv[l].w;
+    const size_t co = (size_t)l * B * kCounterStride;
     uint32_t* hist = as<uint32_t>(c->d_hist) + (size_t)l * B * kMedBins1;
     MedianState* med = as<MedianState>(c->d_med) + (size_t)l * B;
-    {
-      StageScope sc(c, SFM_PROF_HARRIS, st);
-      launch_harris(lvl[l], as<float>(c->d_R), hist, B, h, w, as<float>(c->d_gauss), c->p.gaussian_size,
-                    alpha, st);
-    }
-    {
-      StageScope sc(c, SFM_PROF_MEDIAN, st);
-      launch_median(as<float>(c->d_R), hist, med, as<uint32_t>(c->d_medlist), medcnt + (size_t)l * B * kCounterStride, B,
-                    h, w, st);
-    }
-    {
-      StageScope sc(c, SFM_PROF_NMS, st);
-      launch_nms(as<float>(c->d_R), med, as<uint64_t>(c->d_cand), candcnt + (size_t)l * B * kCounterStride, B, h, w,
-                 c->p.ksize, st);
-    }
     KpList kp;
     size_t ko = (size_t)l * B * std::max(c->kcap, 1);
     kp.x = as<int32_t>(c->d_kpx) + ko;
     kp.y = as<int32_t>(c->d_kpy) + ko;
     kp.conf = as<float>(c->d_kpc) + ko;
     kp.count = as<int32_t>(c->d_lc) + (size_t)l * B;
+    {
+      StageScope sc(c, SFM_PROF_HARRIS, st);
+      launch_harris(lvl[l], as<float>(c->d_R), hist, B, h, w, as<float>(c->d_gauss), c->p.gaussian_size,
+                    alpha, st);
+    }
+    // levels too small to hold ~k window maxima above the median go straight to the exact
+    // path (a size-only decision: no host synchronisation)
+    const bool exact_level = c->exact_select || (int64_t)h * w < (int64_t)64 * c->kcap;
+    {
+      StageScope sc(c, SFM_PROF_MEDIAN, st);
+      launch_select_scan(hist, med, medcnt + co, B, h, w, vmin, exact_level ? 1 : 0, st);
+    }
+    if (!exact_level) {  // certified planes (NaiveSIFT.py:77-120 without the exact median)
+      {
+        StageScope sc(c, SFM_PROF_NMS, st);
+        launch_nms(as<float>(c->d_R), med, as<uint64_t>(c->d_cand), candcnt + co, B, h, w, c->p.ksize, 0, st);
+      }
+      StageScope sc(c, SFM_PROF_TOPK, st);
+      launch_topk(as<uint64_t>(c->d_cand), candcnt + co, as<uint64_t>(c->d_scratch), kp, std::max(c->kcap, 1),
+                  c->kcap, B, h, w, lv[l].fw / 2, med, 0, st);
+    }
+    // exact path for the planes flagged `fallback` (NaiveSIFT.py:77-120); no-ops otherwise
+    {
+      StageScope sc(c, SFM_PROF_MEDIAN, st);
+      launch_median_exact(as<float>(c->d_R), med, as<uint32_t>(c->d_medlist), medcnt + co, B, h, w, st);
+    }
+    {
+      StageScope sc(c, SFM_PROF_NMS, st);
+      launch_nms(as<float>(c->d_R), med, as<uint64_t>(c->d_cand), candcnt2 + co, B, h, w, c->p.ksize, 1, st);
+    }
     StageScope sc(c, SFM_PROF_TOPK, st);
-    launch_topk(as<uint64_t>(c->d_cand), candcnt + (size_t)l * B * kCounterStride, as<uint64_t>(c->d_scratch), kp,
-                std::max(c->kcap, 1), c->kcap, B, h, w, lv[l].fw / 2, st);
+    launch_topk(as<uint64_t>(c->d_cand), candcnt2 + co, as<uint64_t>(c->d_scratch), kp, std::max(c->kcap, 1),
+                c->kcap, B, h, w, lv[l].fw / 2, med, 1, st);
   }
   const int rotate = c->p.mode == SFM_MODE_NAIVE ? 0 : 1;
   for (int l = 0; l < L; ++l) {
@@ -395,6 +417,8 @@ int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out) {
   {
     const char* e = getenv("SFMFEAT_MATCH_DIRECT");
     c->match_direct = e && e[0] == '1';
+    const char* se = getenv("SFMFEAT_SELECT");
+    c->exact_select = se && strcmp(se, "exact") == 0;
   }
   c->cap = (int64_t)c->L * k;
   int gs = p->gaussian_size;
@@ -553,6 +577,19 @@ int32_t sfm_match(sfm_ctx* c, const float* d1, int64_t n1, const float* d2, int6
 int32_t sfm_profile_enable(sfm_ctx* c, int32_t on) {
   if (!c) return SFM_EINVAL;
   c->prof = on != 0;
+  return SFM_OK;
+}
+
+int32_t sfm_debug_select_stats(sfm_ctx* c, int32_t* fallback_planes, int32_t* total_planes) {
+  if (!c || !fallback_planes || !total_planes) return SFM_EINVAL;
+  *fallback_planes = 0;
+  *total_planes = c->L * c->last_B;
+  if (*total_planes == 0) return SFM_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipDeviceSynchronize());
+  std::vector<MedianState> ms((size_t)*total_planes);
+  HIPCHK(c, hipMemcpy(ms.data(), c->d_med.p, ms.size() * sizeof(MedianState), hipMemcpyDeviceToHost));
+  for (const MedianState& m : ms) *fallback_planes += m.fallback ? 1 : 0;
   return SFM_OK;
 }
 

@@ -1,0 +1,135 @@
+"""Multi-process (gloo, CPU) tests of the image-sharding path:
+shard ranges, the point-to-point halo exchange for consecutive pairs, the all-gather of
+slot tables and the round-robin all-pairs deal.  The same functions run over RCCL in
+bench.py; here every rank is a CPU process with fake slot contents keyed by the global
+frame index, so each received slot can be checked exactly."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from sfmfromscratch_amd import distributed as D
+from sfmfromscratch_amd.pipeline import SlotTable
+
+CAP = 16
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _fill_slot(slots, s: int, g: int):
+    """Slot s holds global frame g: count 3 + g % 7, xy / desc derived from g."""
+    slots.count[s] = 3 + g % 7
+    slots.xy[s] = torch.arange(CAP * 2, dtype=torch.int32).view(CAP, 2) + 1000 * g
+    slots.desc[s] = torch.arange(CAP * 128, dtype=torch.float32).view(CAP, 128) * 1e-3 + g
+
+
+def _worker(rank, world, port, n_global, mode, errq):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        lo, hi = D.shard_range(n_global, world, rank)
+        n_local = hi - lo
+        if mode == "halo":
+            slots = SlotTable(torch, n_local + 1, CAP, "cpu")
+            for s in range(n_local):
+                _fill_slot(slots, s, lo + s)
+            D.halo_exchange(dist, slots, n_local, rank, world)
+            pairs = D.local_consecutive_pairs(n_local, rank, world)
+            if rank < world - 1:
+                ref = SlotTable(torch, 1, CAP, "cpu")
+                _fill_slot(ref, 0, hi)
+                assert torch.equal(slots.desc[n_local], ref.desc[0])
+                assert torch.equal(slots.xy[n_local], ref.xy[0])
+                assert int(slots.count[n_local]) == int(ref.count[0])
+            else:
+                assert int(slots.count[n_local]) == 0  # untouched
+            glob = [(lo + int(i), lo + int(j)) for i, j in pairs]
+        else:  # allgather
+            per = -(-n_global // world)
+            slots = SlotTable(torch, per, CAP, "cpu")
+            for s in range(n_local):
+                _fill_slot(slots, s, lo + s)
+            table = D.allgather_slots(dist, slots, per, world)
+            for r in range(world):
+                rlo, rhi = D.shard_range(n_global, world, r)
+                for s in range(rhi - rlo):
+                    ref = SlotTable(torch, 1, CAP, "cpu")
+                    _fill_slot(ref, 0, rlo + s)
+                    assert torch.equal(table.desc[r * per + s], ref.desc[0])
+                    assert int(table.count[r * per + s]) == int(ref.count[0])
+            glob = [tuple(map(int, p)) for p in D.all_pairs_for_rank(n_global, rank, world)]
+        gathered = [None] * world
+        dist.all_gather_object(gathered, glob)
+        if rank == 0:
+            allp = sorted(p for g in gathered for p in g)
+            if mode == "halo":
+                expect = [(i, i + 1) for i in range(n_global - 1)]
+            else:
+                expect = [(i, j) for i in range(n_global) for j in range(i + 1, n_global)]
+            assert allp == expect, (allp, expect)
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as e:  # noqa: BLE001 — report to the parent
+        errq.put(f"rank {rank}: {type(e).__name__}: {e}")
+        raise
+
+
+def _run(world, n_global, mode):
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_global, mode, errq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    alive = [p for p in procs if p.is_alive()]
+    for p in alive:
+        p.kill()
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not alive, "a rank hung"
+    assert not errs and all(p.exitcode == 0 for p in procs), errs
+
+
+@pytest.mark.parametrize("world,n_global", [(2, 8), (2, 7), (3, 10)])
+def test_halo_exchange_consecutive_pairs(world, n_global):
+    _run(world, n_global, "halo")
+
+
+@pytest.mark.parametrize("world,n_global", [(2, 6), (3, 7)])
+def test_allgather_all_pairs(world, n_global):
+    _run(world, n_global, "allgather")
+
+
+def test_shard_range_partitions():
+    for n in range(0, 40):
+        for world in range(1, 9):
+            spans = [D.shard_range(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [h - l for l, h in spans]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        D.shard_range(4, 2, 2)
+
+
+def test_local_pairs_edge_cases():
+    assert D.local_consecutive_pairs(0, 0, 2).shape == (0, 2)
+    assert D.local_consecutive_pairs(1, 0, 2).tolist() == [[0, 1]]
+    assert D.local_consecutive_pairs(3, 1, 2).tolist() == [[0, 1], [1, 2]]
+    assert D.local_consecutive_pairs(3, 0, 1).tolist() == [[0, 1], [1, 2]]
+    a = np.concatenate([D.all_pairs_for_rank(9, r, 4) for r in range(4)])
+    assert len(a) == 36 and len({tuple(p) for p in a.tolist()}) == 36
