@@ -20,9 +20,8 @@ SFM_DEV double pi_edge(int i, int num) {
 }
 
 struct DescLayout {
-  int ws, n, pw, P;
-  size_t off_keys, off_cellv, off_patch, off_ori, off_mag, off_cw, off_cellw, off_cellwt, off_wgh,
-      total;
+  int ws, n, n4, pw, P;
+  size_t off_keys, off_patch, off_ori, off_mag, off_sw, off_cw, off_cellw, off_wgh, total;
 };
 
 __host__ __device__ inline DescLayout desc_layout(int fw, int rotate) {
@@ -34,15 +33,16 @@ __host__ __device__ inline DescLayout desc_layout(int fw, int rotate) {
   int P = 1;
   while (P < L.n) P <<= 1;
   L.P = P;
+  L.n4 = (L.n + 3) & ~3;
   size_t o = 0;
   L.off_keys = o;  o += rotate ? (size_t)P * 8 : 0;
-  L.off_cellv = o; o += 16 * 16 * 8;
   L.off_patch = o; o += (size_t)L.pw * L.pw * 4;
   L.off_ori = o;   o += (size_t)L.n * 4;
   L.off_mag = o;   o += (size_t)L.n * 4;
-  L.off_cw = o;    o += rotate ? (size_t)(L.n + 1) * 4 : 0;
+  o = (o + 15) & ~(size_t)15;
+  L.off_sw = o;    o += rotate ? (size_t)L.n4 * 4 : 0;        // weights in sorted order
+  L.off_cw = o;    o += rotate ? (size_t)(L.n4 + 1) * 4 : 0;  // their prefix sums
   L.off_cellw = o; o += 16 * 17 * 4;
-  L.off_cellwt = o; o += 16 * 16 * 4;
   L.off_wgh = o;   o += 128 * 4;
   o = (o + 15) & ~(size_t)15;
   L.total = o;
@@ -63,13 +63,12 @@ __global__ void __launch_bounds__(64) k_describe(const float* __restrict__ lvl, 
   const int lane = threadIdx.x;
   const DescLayout Ly = desc_layout(fw, rotate);
   uint64_t* s_keys = reinterpret_cast<uint64_t*>(s_raw + Ly.off_keys);
-  double* s_cellv = reinterpret_cast<double*>(s_raw + Ly.off_cellv);
   float* s_patch = reinterpret_cast<float*>(s_raw + Ly.off_patch);
   float* s_ori = reinterpret_cast<float*>(s_raw + Ly.off_ori);
   float* s_mag = reinterpret_cast<float*>(s_raw + Ly.off_mag);
+  float* s_sw = reinterpret_cast<float*>(s_raw + Ly.off_sw);
   float* s_cw = reinterpret_cast<float*>(s_raw + Ly.off_cw);
   float* s_cellw = reinterpret_cast<float*>(s_raw + Ly.off_cellw);
-  float* s_cellwt = reinterpret_cast<float*>(s_raw + Ly.off_cellwt);
   float* s_wgh = reinterpret_cast<float*>(s_raw + Ly.off_wgh);
   __shared__ int s_idx[37];
 
@@ -123,12 +122,28 @@ __global__ void __launch_bounds__(64) k_describe(const float* __restrict__ lvl, 
       s_keys[e] = (e < n) ? (((uint64_t)fkey(s_ori[e]) << 32) | (uint32_t)e) : ~0ull;
     __syncthreads();
     bitonic_sort_u64(s_keys, Ly.P);
+    // weights in sorted order (parallel gather), zero-padded to a multiple of 4
+    for (int m = lane; m < Ly.n4; m += 64) s_sw[m] = (m < n) ? s_mag[(uint32_t)s_keys[m]] : 0.0f;
+    __syncthreads();
+    // np.histogram's float32 cumulative sum: inherently sequential, so one lane adds in
+    // sorted order while its 16-B loads run one step ahead (zero padding adds exactly 0)
     if (lane == 0) {
+      const float4* w4 = reinterpret_cast<const float4*>(s_sw);
+      const int nq = Ly.n4 >> 2;
       float acc = 0.0f;
       s_cw[0] = 0.0f;
-      for (int m = 0; m < n; ++m) {
-        acc = acc + s_mag[(uint32_t)s_keys[m]];
-        s_cw[m + 1] = acc;
+      float4 nxt = w4[0];
+      for (int q = 0; q < nq; ++q) {
+        const float4 cur = nxt;
+        if (q + 1 < nq) nxt = w4[q + 1];
+        acc = acc + cur.x;
+        s_cw[4 * q + 1] = acc;
+        acc = acc + cur.y;
+        s_cw[4 * q + 2] = acc;
+        acc = acc + cur.z;
+        s_cw[4 * q + 3] = acc;
+        acc = acc + cur.w;
+        s_cw[4 * q + 4] = acc;
       }
     }
     if (lane < 37) {
@@ -158,42 +173,62 @@ __global__ void __launch_bounds__(64) k_describe(const float* __restrict__ lvl, 
     dom = (pi_edge(bi, 37) + pi_edge(bi + 1, 37)) / 2.0;
   }
 
-  // 4. 4 x 4 cells of 4 x 4 px from the window's top-left (:68-76), 8 bins each
+  // 4. 4 x 4 cells of 4 x 4 px from the window's top-left (:68-76), 8 bins each.  One lane
+  //    per cell holds its (up to) 16 values in registers in raster order; a Batcher
+  //    odd-even merge network on (value, raster slot) is the stable sort np.histogram's
+  //    cumulative path needs; empty slots (+inf) sort last.
   if (lane < 16) {
     const int r = lane >> 2, cc = lane & 3;
-    double* cv = s_cellv + lane * 16;
+    double cv[16];
+    float wt[16];
+    int sl[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int i = 4 * r + (t >> 2), j = 4 * cc + (t & 3);
+      const bool ok = i < ws && j < ws;
+      const int e = ok ? i * ws + j : 0;
+      const double ov = (double)s_ori[e];
+      cv[t] = ok ? (rotate ? ov - dom : ov) : INFINITY;  // float64 relative angle (:62)
+      wt[t] = ok ? s_mag[e] : 0.0f;
+      sl[t] = t;
+    }
+#pragma unroll
+    for (int p = 1; p < 16; p <<= 1)
+#pragma unroll
+      for (int k = p; k >= 1; k >>= 1)
+#pragma unroll
+        for (int j = k % p; j + k < 16; j += 2 * k)
+#pragma unroll
+          for (int i = 0; i < k; ++i) {
+            const int a = i + j, c = i + j + k;
+            if (c < 16 && a / (2 * p) == c / (2 * p)) {
+              const bool sw = cv[a] > cv[c] || (cv[a] == cv[c] && sl[a] > sl[c]);
+              const double tv = cv[a];
+              cv[a] = sw ? cv[c] : tv;
+              cv[c] = sw ? tv : cv[c];
+              const float tw = wt[a];
+              wt[a] = sw ? wt[c] : tw;
+              wt[c] = sw ? tw : wt[c];
+              const int ts = sl[a];
+              sl[a] = sw ? sl[c] : ts;
+              sl[c] = sw ? ts : sl[c];
+            }
+          }
     float* cw = s_cellw + lane * 17;
-    float* wts = s_cellwt + lane * 16;
-    int cn = 0;
-    for (int i = 4 * r; i < 4 * r + 4 && i < ws; ++i)
-      for (int j = 4 * cc; j < 4 * cc + 4 && j < ws; ++j) {
-        int e = i * ws + j;
-        double ov = (double)s_ori[e];
-        double v = rotate ? ov - dom : ov;   // float64 relative angle (:62)
-        float w = s_mag[e];
-        int p = cn;                           // stable insertion sort by value
-        while (p > 0 && cv[p - 1] > v) {
-          cv[p] = cv[p - 1];
-          wts[p] = wts[p - 1];
-          --p;
-        }
-        cv[p] = v;
-        wts[p] = w;
-        ++cn;
-      }
-    cw[0] = 0.0f;
     float acc = 0.0f;
-    for (int m = 0; m < cn; ++m) {
-      acc = acc + wts[m];
+    cw[0] = 0.0f;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      acc = acc + wt[m];  // empty slots (weight 0) sit after every real value
       cw[m + 1] = acc;
     }
     int idx[9];
 #pragma unroll
     for (int eb = 0; eb < 9; ++eb) {
-      double e = pi_edge(eb, 9);
+      const double e = pi_edge(eb, 9);
       int c = 0;
-      if (eb < 8) { while (c < cn && cv[c] < e) ++c; }
-      else        { while (c < cn && cv[c] <= e) ++c; }
+#pragma unroll
+      for (int m = 0; m < 16; ++m) c += (eb < 8) ? (cv[m] < e ? 1 : 0) : (cv[m] <= e ? 1 : 0);
       idx[eb] = c;
     }
 #pragma unroll
