@@ -6,11 +6,12 @@
 //   1. approximate d^2 = |a|^2 + |b|^2 - 2 a.b for every target with fp16 split operands
 //      (a = hi + lo * 2^-11, three f16 MFMA products hi.hi + (hi.lo + lo.hi), f32
 //      accumulation, operands pre-scaled by 2^8 to keep them out of the f16 subnormal
-//      range) and keep each row's second-smallest approximate value D2~;
-//   2. sweep again and collect every target with d~ <= D2~ + 2 E_i, where E_i bounds
-//      |d~ - d_ref| rigorously (fp16 representation, dropped lo.lo term, f32 accumulation
-//      error <= K u sum|ab|, f32 rounding of d~ and of the reference's own pairwise sum);
-//      any target outside the window is strictly farther than the second nearest;
+//      range), tracking each row's running second-smallest approximate value D2~;
+//   2. in the same sweep collect every target with d~ <= D2~(so far) + 2 E_i, where E_i
+//      bounds |d~ - d_ref| rigorously (fp16 representation, dropped lo.lo term, f32
+//      accumulation error <= K u sum|ab|, f32 rounding of d~ and of the reference's own
+//      pairwise sum); D2~(so far) >= the final D2~, so the collection contains the final
+//      window, and any target outside it is strictly farther than the second nearest;
 //   3. recompute the collected candidates with the reference's exact float32 pairwise
 //      order (8 accumulators) and take (distance, index) minima -> ratio test.
 // Rows whose window overflows the per-row candidate list are recomputed exactly over
@@ -25,9 +26,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kQW = 32;                // query rows per wave
 constexpr int kWaves = 4;              // waves per workgroup
 constexpr int kQB = kQW * kWaves;      // 128 query rows per workgroup
-constexpr int kTT = 32;                // targets per LDS tile
 constexpr int kRowH = 128 + 8;         // padded fp16 row in LDS (272 B): conflict-free b128 reads
-constexpr int kCandCap = 32;           // exact re-rank candidates per query row
+constexpr int kCandCap = 64;           // exact re-rank candidates per query row
 constexpr float kScale = 256.0f;       // operand pre-scale (2^8)
 constexpr float kLoScale = 2048.0f;    // lo part scale (2^11)
 
@@ -131,19 +131,30 @@ SFM_DEV void top2_merge(float& b1, int& j1, float& b2, float ob1, int oj1, float
   }
 }
 
+constexpr int kTT2 = 64;               // targets per LDS stage (two 32-target MFMA sub-tiles)
+constexpr int kStageHalves = kTT2 * kRowH;  // f16 elements per array per stage
+static_assert(kCandCap <= 64, "admission masks are 64-bit at most");
+
+// One workgroup = 4 waves x 32 query rows.  Single sweep over the targets in 64-row stages:
+// the next stage's hi/lo rows are loaded into registers while the current stage's MFMAs
+// run, then stored into the (single) LDS stage buffer.  Per lane the running top-2 of the approximate distances
+// gives a threshold thr = b2~ + 2E that only shrinks, so every target inside the final
+// window (d~ <= b2~_final + 2E) is admitted when visited; the admitted targets are then
+// re-ranked with the reference's exact float32 distance.
 __global__ void __launch_bounds__(256) k_match_mfma(
     const float* __restrict__ desc, const int32_t* __restrict__ count, int64_t cap, int64_t capP,
     const _Float16* __restrict__ hi, const _Float16* __restrict__ lo, const float* __restrict__ norm2,
     const float* __restrict__ rnorm, const unsigned int* __restrict__ imgmax,
     const int32_t* __restrict__ pairs, float ratio, RowBest* __restrict__ rows_out, int max_rows) {
-  __shared__ __attribute__((aligned(16))) _Float16 sHi[kTT][kRowH];
-  __shared__ __attribute__((aligned(16))) _Float16 sLo[kTT][kRowH];
-  __shared__ float sN[kTT];
+  // stage buffer [hi|lo][64][kRowH]; after the sweep the space holds the re-rank scratch
+  __shared__ __attribute__((aligned(16))) _Float16 sT[2][kStageHalves];
+  __shared__ __attribute__((aligned(16))) float sN[kTT2];
   __shared__ uint16_t sCand[kQB][kCandCap];
-  __shared__ float sDex[kQB][kCandCap];
   __shared__ int sCnt[kQB];
-  __shared__ float sRed[3][256];
-  __shared__ int sRedJ[256];
+  float* sDex = reinterpret_cast<float*>(&sT[0][0]);            // [kQB][kCandCap]
+  float* sRed = sDex;                                            // [2][256] (after the re-rank)
+  int* sRedJ = reinterpret_cast<int*>(sRed + 2 * 256);           // [256]
+  static_assert(sizeof(sT) >= (size_t)kQB * kCandCap * 4, "re-rank scratch fits");
 
   const int p = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -167,64 +178,98 @@ __global__ void __launch_bounds__(256) k_match_mfma(
   const float ra = rnorm[(int64_t)i1 * capP + qi];
   const float maxn2 = __uint_as_float(imgmax[i2 * 2 + 0]);
   const float maxrn = __uint_as_float(imgmax[i2 * 2 + 1]);
-  // rigorous |d~ - d_ref| bound (DESIGN.md §Matcher prefilter)
+  // rigorous |d~ - d_ref| bound (matcher exactness)
   const float E = 3.0517578125e-05f * ra * maxrn + 4e-6f * (na + maxn2) + 1.25e-4f;
   for (int i = tid; i < kQB; i += 256) sCnt[i] = 0;
 
-  const int ntiles = (n2 + kTT - 1) / kTT;
+  const int nst = (n2 + kTT2 - 1) / kTT2;
   const int64_t to = (int64_t)i2 * capP * 128;
-  float thr = INFINITY;
-  for (int pass = 0; pass < 2; ++pass) {
-    float b1 = INFINITY, b2 = INFINITY;
-    for (int t = 0; t < ntiles; ++t) {
-      __syncthreads();
-      {  // stage 32 target rows (hi + lo) into LDS: 4 x 16 B per thread
-        const int r = tid >> 3, c = (tid & 7) * 16;
-        const int64_t g = to + (int64_t)(t * kTT + r) * 128 + c;
-        *reinterpret_cast<h8*>(&sHi[r][c]) = *reinterpret_cast<const h8*>(hi + g);
-        *reinterpret_cast<h8*>(&sHi[r][c + 8]) = *reinterpret_cast<const h8*>(hi + g + 8);
-        *reinterpret_cast<h8*>(&sLo[r][c]) = *reinterpret_cast<const h8*>(lo + g);
-        *reinterpret_cast<h8*>(&sLo[r][c + 8]) = *reinterpret_cast<const h8*>(lo + g + 8);
-        if (tid < kTT) sN[tid] = norm2[(int64_t)i2 * capP + t * kTT + tid];
-      }
-      __syncthreads();
-      f32x16 ahh = {}, ax = {};
+  // stage loader: 64 rows x (hi, lo) x 256 B = 32 KB; thread -> (row, 32-B column chunk)
+  const int lr = tid >> 2, lc = (tid & 3) * 32;   // row 0..63, halves 0..127 step 32
+  h8 g[8];
+  auto load_stage = [&](int st) {
+    const int64_t gofs = to + (int64_t)(st * kTT2 + lr) * 128 + lc;  // rows < capP: in bounds
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const h8 thi = *reinterpret_cast<const h8*>(&sHi[lane & 31][kk * 16 + 8 * half]);
-        const h8 tlo = *reinterpret_cast<const h8*>(&sLo[lane & 31][kk * 16 + 8 * half]);
-        ahh = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qhi[kk], ahh, 0, 0, 0);
-        ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qlo[kk], ax, 0, 0, 0);
-        ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(tlo, qhi[kk], ax, 0, 0, 0);
-      }
+    for (int q = 0; q < 4; ++q) {
+      g[q] = *reinterpret_cast<const h8*>(hi + gofs + 8 * q);
+      g[4 + q] = *reinterpret_cast<const h8*>(lo + gofs + 8 * q);
+    }
+  };
+  auto store_stage = [&]() {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int jl = (r & 3) + 8 * (r >> 2) + 4 * half;   // target row within the tile
-        const int j = t * kTT + jl;
-        const float s = (ahh[r] + ax[r] * (1.0f / kLoScale)) * (1.0f / (kScale * kScale));
+    for (int q = 0; q < 4; ++q) {
+      *reinterpret_cast<h8*>(&sT[0][lr * kRowH + lc + 8 * q]) = g[q];
+      *reinterpret_cast<h8*>(&sT[1][lr * kRowH + lc + 8 * q]) = g[4 + q];
+    }
+  };
+  load_stage(0);
+  const float nrm_t0 = (tid < kTT2) ? norm2[(int64_t)i2 * capP + tid] : 0.0f;
+  store_stage();
+  if (tid < kTT2) sN[tid] = nrm_t0;
+
+  float b1 = INFINITY, b2 = INFINITY;
+  for (int st = 0; st < nst; ++st) {
+    __syncthreads();  // stage st visible
+    float nrm_next = 0.0f;
+    if (st + 1 < nst) {
+      load_stage(st + 1);
+      if (tid < kTT2) nrm_next = norm2[(int64_t)i2 * capP + (st + 1) * kTT2 + tid];
+    }
+    const _Float16* tH = &sT[0][0];
+    const _Float16* tL = &sT[1][0];
+    f32x16 ahh0 = {}, ax0 = {}, ahh1 = {}, ax1 = {};
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int ko = kk * 16 + 8 * half;
+      const h8 thi0 = *reinterpret_cast<const h8*>(tH + (lane & 31) * kRowH + ko);
+      const h8 tlo0 = *reinterpret_cast<const h8*>(tL + (lane & 31) * kRowH + ko);
+      const h8 thi1 = *reinterpret_cast<const h8*>(tH + (32 + (lane & 31)) * kRowH + ko);
+      const h8 tlo1 = *reinterpret_cast<const h8*>(tL + (32 + (lane & 31)) * kRowH + ko);
+      ahh0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi0, qhi[kk], ahh0, 0, 0, 0);
+      ahh1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi1, qhi[kk], ahh1, 0, 0, 0);
+      ax0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi0, qlo[kk], ax0, 0, 0, 0);
+      ax1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi1, qlo[kk], ax1, 0, 0, 0);
+      ax0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(tlo0, qhi[kk], ax0, 0, 0, 0);
+      ax1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(tlo1, qhi[kk], ax1, 0, 0, 0);
+    }
+    // per 32-target sub-tile: approximate squared distances of this lane's 16 targets,
+    // running top-2, the row threshold (both halves of the row merged), admission
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      float d[16];
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int jl = 32 * sub + (rr & 3) + 8 * (rr >> 2) + 4 * half;  // target row in the stage
+        const float ah = sub ? ahh1[rr] : ahh0[rr];
+        const float axv = sub ? ax1[rr] : ax0[rr];
+        const float sdot = (ah + axv * (1.0f / kLoScale)) * (1.0f / (kScale * kScale));
         const float t2 = na + sN[jl];
-        const float d = t2 - 2.0f * s;
-        if (j < n2) {
-          if (pass == 0) {
-            if (d < b1) { b2 = b1; b1 = d; }
-            else if (d < b2) b2 = d;
-          } else if (d <= thr && qi < n1) {
-            int slot = atomicAdd(&sCnt[ql], 1);
-            if (slot < kCandCap) sCand[ql][slot] = (uint16_t)j;
-          }
+        const float dv = t2 - 2.0f * sdot;
+        d[rr] = (st * kTT2 + jl < n2) ? dv : INFINITY;
+        b2 = fminf(b2, fmaxf(b1, d[rr]));
+        b1 = fminf(b1, d[rr]);
+      }
+      const float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
+      const float thr = fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + 2.0f * E;
+      uint32_t m = 0;
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) m |= (d[rr] <= thr) ? (1u << rr) : 0u;
+      if (qi < n1 && m) {  // reserve this lane's slots with one LDS atomic, then fill them
+        int slot = atomicAdd(&sCnt[ql], __popc(m));
+        const int jbase = st * kTT2 + 32 * sub + 4 * half;
+        for (; m; m &= m - 1, ++slot) {
+          const int rr = __builtin_ctz(m);
+          if (slot < kCandCap) sCand[ql][slot] = (uint16_t)(jbase + (rr & 3) + 8 * (rr >> 2));
         }
       }
     }
-    if (pass == 0) {
-      // merge the two lanes (halves) that share this query row
-      float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
-      float nb1 = fminf(b1, ob1);
-      float nb2 = fminf(fmaxf(b1, ob1), fminf(b2, ob2));
-      thr = nb2 + 2.0f * E;
-      (void)nb1;
+    if (st + 1 < nst) {
+      __syncthreads();  // every wave is done with this stage's LDS rows
+      store_stage();
+      if (tid < kTT2) sN[tid] = nrm_next;
     }
   }
-  __syncthreads();
+  __syncthreads();  // sweep done: the stage buffers become the re-rank scratch
 
   // exact re-rank of the collected candidates
   int maxc = 0;
@@ -235,23 +280,24 @@ __global__ void __launch_bounds__(256) k_match_mfma(
     const int rl = idx % kQB, slot = idx / kQB;
     const int c = sCnt[rl];
     if (slot < c && c <= kCandCap && row0 + rl < n1)
-      sDex[rl][slot] = exact_sqdist(A + (int64_t)(row0 + rl) * 128, Bd + (int64_t)sCand[rl][slot] * 128);
+      sDex[rl * kCandCap + slot] =
+          exact_sqdist(A + (int64_t)(row0 + rl) * 128, Bd + (int64_t)sCand[rl][slot] * 128);
   }
   __syncthreads();
   if (tid < kQB && row0 + tid < n1 && sCnt[tid] <= kCandCap) {
-    float b1 = INFINITY, b2 = INFINITY;
+    float e1 = INFINITY, e2 = INFINITY;
     int j1 = 0x7fffffff;
     const int c = sCnt[tid];
     for (int s = 0; s < c; ++s) {
-      const float d = sDex[tid][s];
+      const float dd = sDex[tid * kCandCap + s];
       const int j = sCand[tid][s];
-      if (d < b1 || (d == b1 && j < j1)) { b2 = b1; b1 = d; j1 = j; }
-      else if (d < b2) b2 = d;
+      if (dd < e1 || (dd == e1 && j < j1)) { e2 = e1; e1 = dd; j1 = j; }
+      else if (dd < e2) e2 = dd;
     }
     RowBest rb;
     rb.col = -1;
     rb.nndr = 0.0f;
-    const float d1 = sqrtf(b1), d2 = sqrtf(b2);
+    const float d1 = sqrtf(e1), d2 = sqrtf(e2);
     if (d2 > 0.0f) {
       const float nndr = d1 / d2;
       if (nndr <= ratio) { rb.col = j1; rb.nndr = nndr; }
@@ -261,19 +307,19 @@ __global__ void __launch_bounds__(256) k_match_mfma(
   // overflow rows: exact over every target (whole workgroup per row)
   for (int rl = 0; rl < kQB; ++rl) {
     if (sCnt[rl] <= kCandCap || row0 + rl >= n1) continue;  // uniform branch
-    float b1 = INFINITY, b2 = INFINITY;
+    float e1 = INFINITY, e2 = INFINITY;
     int j1 = 0x7fffffff;
     for (int j = tid; j < n2; j += 256) {
-      const float d = exact_sqdist(A + (int64_t)(row0 + rl) * 128, Bd + (int64_t)j * 128);
-      if (d < b1 || (d == b1 && j < j1)) { b2 = b1; b1 = d; j1 = j; }
-      else if (d < b2) b2 = d;
+      const float dd = exact_sqdist(A + (int64_t)(row0 + rl) * 128, Bd + (int64_t)j * 128);
+      if (dd < e1 || (dd == e1 && j < j1)) { e2 = e1; e1 = dd; j1 = j; }
+      else if (dd < e2) e2 = dd;
     }
-    sRed[0][tid] = b1; sRed[1][tid] = b2; sRedJ[tid] = j1;
+    sRed[tid] = e1; sRed[256 + tid] = e2; sRedJ[tid] = j1;  // sDex is dead by now
     __syncthreads();
     if (tid == 0) {
       float B1 = INFINITY, B2 = INFINITY;
       int J1 = 0x7fffffff;
-      for (int t = 0; t < 256; ++t) top2_merge(B1, J1, B2, sRed[0][t], sRedJ[t], sRed[1][t]);
+      for (int t = 0; t < 256; ++t) top2_merge(B1, J1, B2, sRed[t], sRedJ[t], sRed[256 + t]);
       RowBest rb;
       rb.col = -1;
       rb.nndr = 0.0f;
