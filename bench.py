@@ -37,10 +37,15 @@ H, W = 1080, 1920
 PEAK_F32_TFLOPS = 157.3   # MI355X FP32 (vector == matrix) dense peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0     # HBM3E spec
 
-# algorithmic work per pixel / per pair
+# algorithmic work: per pixel for the per-level stages, per pair element for
+# the matcher (GEMM-equivalent 2 n1 n2 128 flop)
 HARRIS_FLOP_PER_PX = 328   # Sobel 2x6 fma (24) + 3 products + 3x49 fma (294) + R (7)
-HARRIS_BYTES_PER_PX = 8    # read the level once, write R once
-MATCH_FLOP_PER_ELEM = 3    # (a-b), square, accumulate: separately rounded f32 ops
+MATCH_FLOP_PER_ELEM = 2    # GEMM-equivalent: one multiply-add per descriptor element pair
+DESC_BYTES_PER_KP = 20 * 20 * 4 + 128 * 4 + 12   # level window + halo read, descriptor + xy/conf written
+KERNELS = {"harris": "k_harris<7>", "match": "k_match_mfma", "describe": "k_describe",
+           "nms": "k_nms_tile<1,0>", "median": "k_med_scan", "topk": "k_topk", "pyramid": "k_down2",
+           "match_prep": "k_match_prep", "match_post": "k_match_compact"}
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")  # tools/pmc_traffic.py
 
 
 def log(*a):
@@ -170,28 +175,43 @@ def main():
     roof = None
     stages = {}
     if prof:
-        # algorithmic work in the timed region
+        # algorithmic work in the timed region, per stage
         levels = [(H >> l, W >> l) for l in range(P_OCT["pyramid_level"])]
         px = sum(h * w for h, w in levels) * B * args.steps
+        px_lo = sum(h * w for h, w in levels[1:]) * B * args.steps
         pair_elems = sum(int(counts[i]) * int(counts[j]) for i, j in pairs_np) * 128 * args.steps
-        work = {
-            "harris": ("mfma", HARRIS_FLOP_PER_PX * px / 1e12, "TFLOP/s", PEAK_F32_TFLOPS,
-                       HARRIS_BYTES_PER_PX * px),
-            "match": ("mfma", MATCH_FLOP_PER_ELEM * pair_elems / 1e12, "TFLOP/s", PEAK_F32_TFLOPS, None),
+        kps = int(counts[:B].sum()) * args.steps
+        work = {  # stage -> (bound, amount, unit, peak)
+            "harris": ("mfma", HARRIS_FLOP_PER_PX * px / 1e12, "TFLOP/s", PEAK_F32_TFLOPS),
+            "match": ("mfma", MATCH_FLOP_PER_ELEM * pair_elems / 1e12, "TFLOP/s", PEAK_F32_TFLOPS),
+            "nms": ("hbm", 4.0 * px / 1e9, "GB/s", PEAK_HBM_GBS),          # one read of R
+            "pyramid": ("hbm", 4.0 * px_lo * 5 / 1e9, "GB/s", PEAK_HBM_GBS),  # read 4 px, write 1
+            "describe": ("hbm", DESC_BYTES_PER_KP * kps / 1e9, "GB/s", PEAK_HBM_GBS),
         }
-        stages = {k: {"ms_total": round(v[0], 3), "launches": v[1]} for k, v in prof.items() if v[1]}
-        dom = max(prof, key=lambda k: prof[k][0])
-        if dom in work:
-            bound, amount, unit, peak, _ = work[dom]
-            ms, n = prof[dom]
-            achieved = amount / (ms / 1e3)
-            roof = {"kernel": {"harris": "k_harris<7>", "match": "k_match_rows"}[dom], "bound": bound,
-                    "achieved": round(achieved, 3), "peak": peak, "unit": unit,
-                    "frac": round(achieved / peak, 4), "traffic": None,
-                    "avg_launch_ms": round(ms / max(n, 1), 4), "launches": n}
-        else:
-            roof = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                    "frac": None, "traffic": None}
+        traffic = {}
+        if os.path.exists(TRAFFIC_FILE):
+            with open(TRAFFIC_FILE) as f:
+                traffic = json.load(f).get("bytes_per_launch", {})
+        for k, (ms, n) in prof.items():
+            if not n:
+                continue
+            st = {"ms_total": round(ms, 3), "launches": n}
+            if k in work:
+                bound, amount, unit, peak = work[k]
+                ach = amount / (ms / 1e3)
+                st.update({"bound": bound, "achieved": round(ach, 3), "unit": unit, "frac": round(ach / peak, 4)})
+            stages[k] = st
+        dom = max((k for k in prof if k in work and prof[k][1]), key=lambda k: prof[k][0])
+        bound, amount, unit, peak = work[dom]
+        ms, n = prof[dom]
+        achieved = amount / (ms / 1e3)
+        kname = KERNELS[dom]
+        tr = traffic.get(kname)
+        roof = {"kernel": kname, "stage": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak,
+                "unit": unit, "frac": round(achieved / peak, 4), "traffic": tr,
+                "avg_launch_ms": round(ms / max(n, 1), 4), "launches": n}
+        if tr is not None:
+            roof["traffic_note"] = "HBM bytes per launch, rocprofv3 PMC (profiles/pmc_traffic.json)"
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:

@@ -131,9 +131,11 @@ int32_t sfm_match(sfm_ctx* ctx, const float* d1, int64_t n1, const float* d2, in
                   float ratio, int64_t* matches, float* conf, int64_t cap, int64_t* k_out);
 
 /* ---------------- device-resident batch API (throughput path) ----------------
- * All pointers are device pointers on the context's device; `stream` is a
- * hipStream_t (NULL = the context's own stream).  The calls are asynchronous with
- * respect to the host: results are valid once the stream has been synchronised.
+ * All pointers are device pointers on the context's device; `stream` is the
+ * hipStream_t the work is enqueued on, exactly as given (NULL = HIP's null stream, as
+ * in the HIP API — so a caller on PyTorch's default stream passes its handle, 0, and
+ * stays ordered with its own work).  The calls are asynchronous with respect to the
+ * host: results are valid once the stream has been synchronised.
  * Workspace is owned by the context; call sfm_reserve() once with the largest batch
  * so that the batch calls perform no device allocation (hipGraph-capturable).
  *

@@ -217,38 +217,50 @@ __global__ void __launch_bounds__(256) k_match_mfma(
     }
     const _Float16* tH = &sT[0][0];
     const _Float16* tL = &sT[1][0];
-    f32x16 ahh0 = {}, ax0 = {}, ahh1 = {}, ax1 = {};
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int ko = kk * 16 + 8 * half;
-      const h8 thi0 = *reinterpret_cast<const h8*>(tH + (lane & 31) * kRowH + ko);
-      const h8 tlo0 = *reinterpret_cast<const h8*>(tL + (lane & 31) * kRowH + ko);
-      const h8 thi1 = *reinterpret_cast<const h8*>(tH + (32 + (lane & 31)) * kRowH + ko);
-      const h8 tlo1 = *reinterpret_cast<const h8*>(tL + (32 + (lane & 31)) * kRowH + ko);
-      ahh0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi0, qhi[kk], ahh0, 0, 0, 0);
-      ahh1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi1, qhi[kk], ahh1, 0, 0, 0);
-      ax0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi0, qlo[kk], ax0, 0, 0, 0);
-      ax1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi1, qlo[kk], ax1, 0, 0, 0);
-      ax0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(tlo0, qhi[kk], ax0, 0, 0, 0);
-      ax1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(tlo1, qhi[kk], ax1, 0, 0, 0);
-    }
-    // per 32-target sub-tile: approximate squared distances of this lane's 16 targets,
-    // running top-2, the row threshold (both halves of the row merged), admission
+    const bool full = st * kTT2 + kTT2 <= n2;  // uniform: only the last stage is partial
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
+      // 32 targets x 32 queries: hi.hi into ahh, hi.lo + lo.hi into ax (one chain each)
+      f32x16 ahh = {}, ax = {};
+      const int trow = (32 * sub + (lane & 31)) * kRowH;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const int ko = kk * 16 + 8 * half;
+        const h8 thi = *reinterpret_cast<const h8*>(tH + trow + ko);
+        const h8 tlo = *reinterpret_cast<const h8*>(tL + trow + ko);
+        ahh = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qhi[kk], ahh, 0, 0, 0);
+        ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qlo[kk], ax, 0, 0, 0);
+        ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(tlo, qhi[kk], ax, 0, 0, 0);
+      }
+      // d~ = na + nb - 2 a.b with a.b = (ahh + ax 2^-11) 2^-16: two fmas by exact powers
+      // of two (each rounding is covered by E's 4e-6 (na + nb) term)
       float d[16];
 #pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 nb4 = *reinterpret_cast<const float4*>(&sN[32 * sub + 8 * g4 + 4 * half]);
+        const float nbv[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rr = 4 * g4 + e;
+          const float t2 = na + nbv[e];
+          d[rr] = __builtin_fmaf(ax[rr], -1.4901161193847656e-08f /* -2^-26 */,
+                                 __builtin_fmaf(ahh[rr], -3.0517578125e-05f /* -2^-15 */, t2));
+        }
+      }
+      if (!full) {
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) {
+          const int j = st * kTT2 + 32 * sub + (rr & 3) + 8 * (rr >> 2) + 4 * half;
+          d[rr] = j < n2 ? d[rr] : INFINITY;
+        }
+      }
+      // running top-2 (b1 <= b2): b2 = med3(b1, b2, d), b1 = min(b1, d)
+#pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
-        const int jl = 32 * sub + (rr & 3) + 8 * (rr >> 2) + 4 * half;  // target row in the stage
-        const float ah = sub ? ahh1[rr] : ahh0[rr];
-        const float axv = sub ? ax1[rr] : ax0[rr];
-        const float sdot = (ah + axv * (1.0f / kLoScale)) * (1.0f / (kScale * kScale));
-        const float t2 = na + sN[jl];
-        const float dv = t2 - 2.0f * sdot;
-        d[rr] = (st * kTT2 + jl < n2) ? dv : INFINITY;
-        b2 = fminf(b2, fmaxf(b1, d[rr]));
+        b2 = __builtin_amdgcn_fmed3f(b1, b2, d[rr]);
         b1 = fminf(b1, d[rr]);
       }
+      // the row's threshold (both halves merged), then admission
       const float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
       const float thr = fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + 2.0f * E;
       uint32_t m = 0;

@@ -473,7 +473,7 @@ int32_t sfm_extract_batch_dev(sfm_ctx* c, const float* imgs, int32_t B, int32_t 
                               int32_t* xy, float* desc, int32_t* count, int64_t cap, void* stream) {
   if (!c || !imgs || !xy || !desc || !count) return SFM_EINVAL;
   HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t st = (hipStream_t)stream;  // exactly the caller's stream (NULL = null stream)
   return extract_impl(c, imgs, B, H, W, xy, desc, nullptr, count, cap, st);
 }
 
@@ -481,7 +481,7 @@ int32_t sfm_extract_batch_u8_dev(sfm_ctx* c, const uint8_t* imgs, int32_t B, int
                                  int32_t* xy, float* desc, int32_t* count, int64_t cap, void* stream) {
   if (!c || !imgs || !xy || !desc || !count || B < 1 || H < 1 || W < 1) return SFM_EINVAL;
   HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t st = (hipStream_t)stream;  // exactly the caller's stream (NULL = null stream)
   int rc = reserve_impl(c, B, H, W);
   if (rc) return rc;
   launch_u8_to_f32(imgs, as<float>(c->d_img0), (int64_t)B * H * W, st);
@@ -623,7 +623,7 @@ int32_t sfm_match_pairs_dev(sfm_ctx* c, const float* desc, const int32_t* count,
   if (!c || !desc || !count || !pairs || !matches || !conf || !nmatch || nimg < 1 || P < 0)
     return SFM_EINVAL;
   HIPCHK(c, hipSetDevice(c->device));
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t st = (hipStream_t)stream;  // exactly the caller's stream (NULL = null stream)
   return match_impl(c, desc, count, nimg, cap, pairs, P, ratio, matches, conf, nmatch, st);
 }
 
