@@ -28,5 +28,13 @@ if [ "${SKIP_PROF:-0}" != 1 ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
        python bench.py --steps 5 --warmup 2 --cpu-sample 0 --no-profile || exit 1
   find $OUT/prof_$TAG -name "*kernel_stats.csv" | head -3
+  python tools/trace_summary.py $OUT/prof_$TAG > $OUT/trace_summary_$TAG.txt 2>&1 || true
+fi
+if [ "${PMC:-0}" = 1 ]; then  # HBM traffic: FETCH_SIZE and WRITE_SIZE in separate passes, no tracing
+  for c in FETCH_SIZE WRITE_SIZE; do
+    step pmc_$c 600 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_${TAG}_$c -o run -- \
+         python bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-profile || exit 1
+  done
+  python tools/pmc_traffic.py $OUT/pmc_${TAG}_FETCH_SIZE $OUT/pmc_${TAG}_WRITE_SIZE $OUT/pmc_traffic_$TAG.json
 fi
 echo done
