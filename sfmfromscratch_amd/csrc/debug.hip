@@ -65,7 +65,8 @@ int32_t sfm_debug_harris(int32_t device, const float* gauss, int32_t gs, double 
     (void)hipMemcpy(d_g, gauss, 4 * gs * gs, hipMemcpyHostToDevice);
     (void)hipMemset(d_hist, 0, 4 * kMedBins1);
     (void)hipMemset(d_cnt, 0, 16 * kCounterStride);
-    launch_harris(d_img, d_R, d_hist, 1, H, W, d_g, gs, (float)alpha, 0);
+    launch_harris(d_img, d_R, d_hist, 1, H, W, d_g, gs, (float)alpha, SelectScan{nullptr, nullptr, nullptr, 0, 0},
+                  0);
     launch_select_scan(d_hist, d_med, d_cnt, 1, H, W, 0, /*force_exact=*/1, 0);
     launch_median_exact(d_R, d_med, d_list, d_cnt, 1, H, W, 0);
     launch_nms(d_R, d_med, d_cand, d_cnt + kCounterStride, 1, H, W, ksize, 1, 0);

@@ -39,7 +39,8 @@ template <int KS, int ABL = 0>
 __global__ void __launch_bounds__(256) k_harris(const float* __restrict__ lvl, float* __restrict__ Rout,
                                                 uint32_t* __restrict__ hist_g, int H, int W,
                                                 int tiles_x, int ntiles,
-                                                const float* __restrict__ gk, float alpha) {
+                                                const float* __restrict__ gk, float alpha,
+                                                SelectScan scan) {
   constexpr int GA = KS / 2;
   constexpr int PW = kHT_W + KS - 1;        // product tile width
   constexpr int PH = kHT_H + KS - 1;        // product tile height
@@ -61,6 +62,7 @@ __global__ void __launch_bounds__(256) k_harris(const float* __restrict__ lvl, f
   __shared__ __attribute__((aligned(16))) float s_prod[3][PH][PWP];
   __shared__ __attribute__((aligned(16))) float s_img[IH][IWP];
   __shared__ uint32_t s_hist[kMedBins1];  // digit-1 histogram, flushed once per workgroup
+  __shared__ uint32_t s_last, s_red[8];
 
   const int tid = threadIdx.x;
   const int b = blockIdx.y;
@@ -274,11 +276,24 @@ __global__ void __launch_bounds__(256) k_harris(const float* __restrict__ lvl, f
     uint32_t c = s_hist[i];
     if (c) atomicAdd(&hg[i], c);
   }
+  if (scan.state == nullptr) return;
+  // The last workgroup of this plane to finish runs the select scan.  The
+  // flushes are device-scope atomics, performed at the memory side: waiting for their
+  // acknowledgement (vmcnt) orders them before the arrival count without the L2
+  // write-back a __threadfence() costs; the scan reads the histogram with agent-scope
+  // atomic loads.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(&scan.done[(int64_t)b * kCounterStride], 1ull) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!s_last) return;
+  select_scan_plane(hg, scan.state + b, scan.list_count + (int64_t)b * kCounterStride, (int64_t)H * W,
+                    scan.vmin, scan.force_exact, s_red);
 }
 
 template <int KS, int ABL = 0>
 static void launch_ks(const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
-                      const float* gk, float alpha, hipStream_t st) {
+                      const float* gk, float alpha, SelectScan scan, hipStream_t st) {
   int tiles_x = (W + kHT_W - 1) / kHT_W;
   int tiles_y = (H + kHT_H - 1) / kHT_H;
   int ntiles = tiles_x * tiles_y;
@@ -286,24 +301,24 @@ static void launch_ks(const float* lvl, float* R, uint32_t* hist, int B, int H, 
   // digit histogram is flushed once per workgroup instead of once per tile
   int per_plane = std::max(1, std::min(ntiles, 768 / std::max(B, 1)));
   hipLaunchKernelGGL((k_harris<KS, ABL>), dim3(per_plane, B), dim3(256), 0, st, lvl, R, hist, H, W,
-                     tiles_x, ntiles, gk, alpha);
+                     tiles_x, ntiles, gk, alpha, scan);
 }
 
 void launch_harris(const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
-                   const float* d_gauss, int ks, float alpha, hipStream_t st) {
+                   const float* d_gauss, int ks, float alpha, SelectScan scan, hipStream_t st) {
   switch (ks) {
-    case 1: launch_ks<1>(lvl, R, hist, B, H, W, d_gauss, alpha, st); break;
-    case 2: launch_ks<2>(lvl, R, hist, B, H, W, d_gauss, alpha, st); break;
-    case 3: launch_ks<3>(lvl, R, hist, B, H, W, d_gauss, alpha, st); break;
-    case 4: launch_ks<4>(lvl, R, hist, B, H, W, d_gauss, alpha, st); break;
-    case 5: launch_ks<5>(lvl, R, hist, B, H, W, d_gauss, alpha, st); break;
-    case 6: launch_ks<6>(lvl, R, hist, B, H, W, d_gauss, alpha, st); break;
-    case 7: launch_ks<7>(lvl, R, hist, B, H, W, d_gauss, alpha, st); break;
-    case 8: launch_ks<8>(lvl, R, hist, B, H, W, d_gauss, alpha, st); break;
-    case 9: launch_ks<9>(lvl, R, hist, B, H, W, d_gauss, alpha, st); break;
-    case 11: launch_ks<11>(lvl, R, hist, B, H, W, d_gauss, alpha, st); break;
-    case 13: launch_ks<13>(lvl, R, hist, B, H, W, d_gauss, alpha, st); break;
-    case 15: launch_ks<15>(lvl, R, hist, B, H, W, d_gauss, alpha, st); break;
+    case 1: launch_ks<1>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 2: launch_ks<2>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 3: launch_ks<3>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 4: launch_ks<4>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 5: launch_ks<5>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 6: launch_ks<6>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 7: launch_ks<7>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 8: launch_ks<8>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 9: launch_ks<9>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 11: launch_ks<11>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 13: launch_ks<13>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 15: launch_ks<15>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
     default: break;  // rejected at context creation
   }
 }
@@ -314,14 +329,15 @@ float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, 
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
+  const SelectScan none{nullptr, nullptr, nullptr, 0, 0};
   auto run = [&]() {
     switch (abl) {
-      case 1: launch_ks<7, 1>(lvl, R, hist, B, H, W, gk, alpha, 0); break;
-      case 2: launch_ks<7, 2>(lvl, R, hist, B, H, W, gk, alpha, 0); break;
-      case 3: launch_ks<7, 3>(lvl, R, hist, B, H, W, gk, alpha, 0); break;
-      case 4: launch_ks<7, 4>(lvl, R, hist, B, H, W, gk, alpha, 0); break;
-      case 5: launch_ks<7, 5>(lvl, R, hist, B, H, W, gk, alpha, 0); break;
-      default: launch_ks<7, 0>(lvl, R, hist, B, H, W, gk, alpha, 0); break;
+      case 1: launch_ks<7, 1>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
+      case 2: launch_ks<7, 2>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
+      case 3: launch_ks<7, 3>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
+      case 4: launch_ks<7, 4>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
+      case 5: launch_ks<7, 5>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
+      default: launch_ks<7, 0>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
     }
   };
   run();

@@ -42,6 +42,84 @@ struct MedianState {
   uint32_t fallback;    // 1: this plane takes the exact path
 };
 
+// Buckets from 2^126 up (and inf / NaN) never certify: (lo + hi) / 2 could overflow.
+constexpr uint32_t kHugeBucket = 0x7F4u;
+
+// Per-plane select scan (median.hip k_med_scan; fused into the Harris kernel's last
+// workgroup of each plane): from the digit-1 histogram, the buckets holding the two
+// middle ranks (exact-median state) and the certified-select thresholds.  Needs exactly
+// 256 threads (8 bins each, one prefix pass for all three ranks); s_red holds 8 u32.
+// `hist` is read with agent-scope atomic loads so a fused caller sees every workgroup's
+// flush (L2 is per XCD); the 8 loads per thread are issued together.
+SFM_DEV void select_scan_plane(const uint32_t* hist, MedianState* st, unsigned long long* list_count,
+                               int64_t n, int64_t vmin, int force_exact, uint32_t* s_red) {
+  static_assert(kMedBins1 == 256 * 8, "select scan: 8 bins per thread");
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  uint32_t v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = __hip_atomic_load(hist + 8 * tid + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t local = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) local += v[j];
+  uint32_t x = local;  // inclusive scan within the wave
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_red[wid] = x;
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (int w = 0; w < wid; ++w) wbase += s_red[w];
+  const uint32_t excl = wbase + x - local;  // values in bins below this thread's first bin
+  __syncthreads();
+  const uint32_t k1 = (n % 2 == 1) ? (uint32_t)(n / 2) : (uint32_t)(n / 2 - 1);
+  const uint32_t k2 = (uint32_t)(n / 2);
+  const uint32_t kv = n > vmin ? (uint32_t)(n - vmin) : 0u;  // vmin-th largest value
+  const uint32_t ranks[3] = {k1, k2, kv};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const uint32_t r = ranks[q];
+    if (r >= excl && r < excl + local) {  // exactly one thread owns each rank
+      uint32_t c = excl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (r >= c && r < c + v[j]) {
+          s_red[2 * q] = (uint32_t)(8 * tid + j);
+          s_red[2 * q + 1] = r - c;  // residual rank inside the bucket
+        }
+        c += v[j];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t b1 = s_red[0], r1 = s_red[1], b2 = s_red[2], r2 = s_red[3];
+    // candidate threshold: the bucket holding the vmin-th largest value (so >= vmin values
+    // lie at or above it), at least the median's lower bucket b1 (nothing below certifies)
+    const uint32_t tb = max(n > vmin ? s_red[4] : 0u, b1);
+    const bool certifiable = !force_exact && b2 < kHugeBucket;
+    st->tnms = tb << (32 - kMedBits1);
+    st->tcert = certifiable ? (b2 + 1) << (32 - kMedBits1) : 0xffffffffu;
+    st->fallback = certifiable ? 0u : 1u;
+    st->bucket[0] = b1;
+    st->bucket[1] = b2;
+    st->rank[0] = r1;
+    st->rank[1] = r2;
+    st->odd = (uint32_t)(n % 2);
+    *list_count = 0ull;
+  }
+}
+
+// Arguments of the select scan fused into the Harris launch (state == nullptr: not fused).
+struct SelectScan {
+  MedianState* state;                  // [B]
+  unsigned long long* list_count;      // [B], stride kCounterStride
+  unsigned long long* done;            // [B], stride kCounterStride: workgroup arrivals (zeroed)
+  int64_t vmin;
+  int force_exact;
+};
+
 // Per-plane keypoint list produced by the top-k kernel (level coordinates).
 struct KpList {
   int32_t* x;      // [planes][kcap]
@@ -55,9 +133,10 @@ void launch_u8_to_f32(const uint8_t* src, float* dst, int64_t n, hipStream_t st)
 void launch_resize(const float* src, int sh, int sw, float* dst, int dh, int dw, int B,
                    hipStream_t st);
 
-// harris.hip: R map + first median digit histogram (hist zeroed by the caller).
+// harris.hip: R map + first median digit histogram (hist zeroed by the caller); with
+// scan.state set, the last workgroup of each plane also runs select_scan_plane.
 void launch_harris(const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
-                   const float* d_gauss, int ks, float alpha, hipStream_t st);
+                   const float* d_gauss, int ks, float alpha, SelectScan scan, hipStream_t st);
 
 float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
                            const float* gk, float alpha, int iters);

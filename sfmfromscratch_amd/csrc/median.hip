@@ -14,48 +14,15 @@
 
 namespace sfm {
 
-// Buckets from 2^126 up (and inf / NaN) never certify: (lo + hi) / 2 could overflow.
-constexpr uint32_t kHugeBucket = 0x7F4u;
-
+// Stand-alone select scan (the diagnostic path; extraction fuses it into k_harris).
 __global__ void __launch_bounds__(256) k_med_scan(const uint32_t* __restrict__ hist,
                                                   MedianState* __restrict__ st,
                                                   unsigned long long* __restrict__ list_count,
                                                   int64_t n, int64_t vmin, int force_exact) {
-  __shared__ uint32_t s_h[kHistBins];
-  __shared__ uint32_t s_scan[256];
-  __shared__ uint32_t s_out[2];
+  __shared__ uint32_t s_red[8];
   const int b = blockIdx.x;
-  for (int i = threadIdx.x; i < kHistBins; i += 256)
-    s_h[i] = i < kMedBins1 ? hist[(int64_t)b * kMedBins1 + i] : 0u;
-  __syncthreads();
-  uint32_t k1 = (n % 2 == 1) ? (uint32_t)(n / 2) : (uint32_t)(n / 2 - 1);
-  uint32_t k2 = (uint32_t)(n / 2);
-  find_bin(s_h, kHistBins, k1, s_scan, s_out);
-  uint32_t b1 = s_out[0], r1 = k1 - s_out[1];
-  __syncthreads();
-  find_bin(s_h, kHistBins, k2, s_scan, s_out);
-  uint32_t b2 = s_out[0], r2 = k2 - s_out[1];
-  __syncthreads();
-  // candidate threshold: the bucket holding the vmin-th largest value (so >= vmin values
-  // lie at or above it), at least the median's lower bucket b1 (nothing below certifies)
-  uint32_t tb = 0;
-  if (n > vmin) {
-    find_bin(s_h, kHistBins, (uint32_t)(n - vmin), s_scan, s_out);
-    tb = s_out[0];
-  }
-  tb = max(tb, b1);
-  const bool certifiable = !force_exact && b2 < kHugeBucket;
-  if (threadIdx.x == 0) {
-    st[b].tnms = tb << (32 - kMedBits1);
-    st[b].tcert = certifiable ? (b2 + 1) << (32 - kMedBits1) : 0xffffffffu;
-    st[b].fallback = certifiable ? 0u : 1u;
-    st[b].bucket[0] = b1;
-    st[b].bucket[1] = b2;
-    st[b].rank[0] = r1;
-    st[b].rank[1] = r2;
-    st[b].odd = (uint32_t)(n % 2);
-    list_count[(int64_t)b * kCounterStride] = 0ull;
-  }
+  select_scan_plane(hist + (int64_t)b * kMedBins1, st + b, list_count + (int64_t)b * kCounterStride, n, vmin,
+                    force_exact, s_red);
 }
 
 constexpr int kCollectPerThread = 16;

@@ -13,7 +13,7 @@
 // "R == window max" is tested as "no cell of the clipped window is larger"; out-of-image
 // cells hold -inf and never win.
 //
-// k_nms_tile (ksize <= 9): persistent workgroups walk 64 x 32 tiles of one plane; the tile
+// k_nms_tile (ksize <= 9): persistent workgroups walk 64 x 64 tiles of one plane; the tile
 // + halo (72-float rows, 16-B aligned) is loaded with 16-B loads into registers one tile
 // ahead, then staged through LDS.  HBM-bound: ~1.2 reads of R.
 // k_nms_generic (larger ksize): separable window max on an LDS tile.
@@ -24,10 +24,11 @@
 namespace sfm {
 
 constexpr int kNT_W = 64;
-constexpr int kNT_H = 32;
+constexpr int kNT_H = 32;          // k_nms_generic tile height
+constexpr int kTT_H = 64;          // k_nms_tile tile height (more bytes in flight per workgroup)
 constexpr int kNmsBlocksPerPlane = 64;
 
-template <int KH, int MODE>
+template <int KH, int MODE, bool VEC>  // VEC: W % 4 == 0 (16-B aligned rows and planes)
 __global__ void __launch_bounds__(256) k_nms_tile(const float* __restrict__ R,
                                                   const MedianState* __restrict__ st,
                                                   uint64_t* __restrict__ cand,
@@ -36,7 +37,7 @@ __global__ void __launch_bounds__(256) k_nms_tile(const float* __restrict__ R,
   static_assert(KH <= 4, "72-float rows hold a 4-column halo");
   constexpr int LW = 72;                // tile columns tx0-4 .. tx0+67
   constexpr int LW4 = LW / 4;
-  constexpr int LH = kNT_H + 2 * KH;
+  constexpr int LH = kTT_H + 2 * KH;
   constexpr int NV4 = LH * LW4;
   constexpr int PER = (NV4 + 255) / 256;
   __shared__ __attribute__((aligned(16))) float s_t[LH][LW];
@@ -50,56 +51,67 @@ __global__ void __launch_bounds__(256) k_nms_tile(const float* __restrict__ R,
   const float med = st[b].median;
   const int64_t n = (int64_t)H * W;
   const float* Rp = R + (int64_t)b * n;
-  const bool vec = (W & 3) == 0;  // 16-B aligned rows (the plane base too: n % 4 == 0)
 
+  // loads are unconditional (clamped addresses) and masked afterwards, so all of them are
+  // in flight together — a branch around a load makes the compiler wait on it in place
+  // (and masked only when stored to LDS, one tile later, so nothing waits on them early)
   float4 t[PER];
+  uint32_t okm = 0;  // VEC: bit k = slot k inside the image; !VEC: 4 bits per slot
   auto prefetch = [&](int tile) {
     const int x0 = (tile % tiles_x) * kNT_W - 4;
-    const int y0 = (tile / tiles_x) * kNT_H - KH;
+    const int y0 = (tile / tiles_x) * kTT_H - KH;
+    okm = 0;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      const int e = tid + 256 * k;
+      const int e = min(tid + 256 * k, NV4 - 1);
       const int row = e / LW4, c4 = e - row * LW4;
       const int gy = y0 + row, gx = x0 + 4 * c4;
-      const bool rowok = e < NV4 && gy >= 0 && gy < H;
-      const int yc = min(max(gy, 0), H - 1);
-      if (vec) {
-        const int xc = min(max(gx, 0), W - 4);
-        const float4 v = *reinterpret_cast<const float4*>(Rp + (int64_t)yc * W + xc);
-        const bool ok = rowok && gx >= 0 && gx < W;  // W % 4 == 0: a float4 is all in or all out
-        t[k] = ok ? v : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      const bool rowok = gy >= 0 && gy < H;
+      const float* rp = Rp + (int64_t)min(max(gy, 0), H - 1) * W;
+      if (VEC) {
+        t[k] = *reinterpret_cast<const float4*>(rp + min(max(gx, 0), W - 4));
+        okm |= (rowok && gx >= 0 && gx < W) ? (1u << k) : 0u;  // W % 4 == 0: all in or all out
       } else {
         float q[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int x = gx + j;
-          const float v = Rp[(int64_t)yc * W + min(max(x, 0), W - 1)];
-          q[j] = (rowok && x >= 0 && x < W) ? v : -INFINITY;
+          q[j] = rp[min(max(x, 0), W - 1)];
+          okm |= (rowok && x >= 0 && x < W) ? (1u << (4 * k + j)) : 0u;
         }
         t[k] = make_float4(q[0], q[1], q[2], q[3]);
       }
     }
   };
+  static_assert(VEC ? PER <= 32 : PER <= 8, "prefetch mask bits");
 
-  const int r = tid >> 3;          // output row in the tile
-  const int c0 = (tid & 7) * 8;    // 8 output columns
+  const int c0 = (tid & 7) * 8;    // 8 output columns, rows tid >> 3 and (tid >> 3) + 32
   if (blockIdx.x < ntiles) prefetch(blockIdx.x);
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int tx0 = (tile % tiles_x) * kNT_W;
-    const int ty0 = (tile / tiles_x) * kNT_H;
+    const int ty0 = (tile / tiles_x) * kTT_H;
     __syncthreads();  // previous tile's LDS reads done
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int e = tid + 256 * k;
-      if (e < NV4) reinterpret_cast<float4*>(&s_t[0][0])[e] = t[k];
+      float4 v = t[k];
+      if (VEC) {
+        if (!((okm >> k) & 1u)) v = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      } else {
+        v.x = ((okm >> (4 * k)) & 1u) ? v.x : -INFINITY;
+        v.y = ((okm >> (4 * k + 1)) & 1u) ? v.y : -INFINITY;
+        v.z = ((okm >> (4 * k + 2)) & 1u) ? v.z : -INFINITY;
+        v.w = ((okm >> (4 * k + 3)) & 1u) ? v.w : -INFINITY;
+      }
+      if (e < NV4) reinterpret_cast<float4*>(&s_t[0][0])[e] = v;
     }
     __syncthreads();
     if (tile + (int)gridDim.x < ntiles) prefetch(tile + gridDim.x);
     uint32_t flags = 0;
-    float vals[8];
+    float vals[16];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int c = c0 + q;
+    for (int q = 0; q < 16; ++q) {
+      const int r = (tid >> 3) + 32 * (q >> 3), c = c0 + (q & 7);
       const float v = s_t[r + KH][4 + c];
       vals[q] = v;
       const bool inside = ty0 + r < H && tx0 + c < W;
@@ -123,9 +135,11 @@ __global__ void __launch_bounds__(256) k_nms_tile(const float* __restrict__ R,
                                         s_wsum, &s_base);
       uint64_t* out = cand + (int64_t)b * n + slot;
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (flags & (1u << q))
-          *out++ = ((uint64_t)(~fkey(vals[q])) << 32) | (uint32_t)((ty0 + r) * W + tx0 + c0 + q);
+      for (int q = 0; q < 16; ++q)
+        if (flags & (1u << q)) {
+          const int r = (tid >> 3) + 32 * (q >> 3), c = c0 + (q & 7);
+          *out++ = ((uint64_t)(~fkey(vals[q])) << 32) | (uint32_t)((ty0 + r) * W + tx0 + c);
+        }
     }
   }
 }
@@ -202,12 +216,18 @@ __global__ void __launch_bounds__(256) k_nms_generic(const float* __restrict__ R
 
 template <int KH>
 static void launch_tile(const float* R, const MedianState* state, uint64_t* cand, unsigned long long* cnt,
-                        int B, int H, int W, int tiles_x, int ntiles, int mode, hipStream_t st) {
+                        int B, int H, int W, int tiles_x, int mode, hipStream_t st) {
+  const int ntiles = tiles_x * ((H + kTT_H - 1) / kTT_H);
   dim3 grid(std::min(ntiles, kNmsBlocksPerPlane), B);
-  if (mode == 0)
-    hipLaunchKernelGGL((k_nms_tile<KH, 0>), grid, dim3(256), 0, st, R, state, cand, cnt, H, W, tiles_x, ntiles);
+  const bool vec = (W & 3) == 0;
+  if (mode == 0 && vec)
+    hipLaunchKernelGGL((k_nms_tile<KH, 0, true>), grid, dim3(256), 0, st, R, state, cand, cnt, H, W, tiles_x, ntiles);
+  else if (mode == 0)
+    hipLaunchKernelGGL((k_nms_tile<KH, 0, false>), grid, dim3(256), 0, st, R, state, cand, cnt, H, W, tiles_x, ntiles);
+  else if (vec)
+    hipLaunchKernelGGL((k_nms_tile<KH, 1, true>), grid, dim3(256), 0, st, R, state, cand, cnt, H, W, tiles_x, ntiles);
   else
-    hipLaunchKernelGGL((k_nms_tile<KH, 1>), grid, dim3(256), 0, st, R, state, cand, cnt, H, W, tiles_x, ntiles);
+    hipLaunchKernelGGL((k_nms_tile<KH, 1, false>), grid, dim3(256), 0, st, R, state, cand, cnt, H, W, tiles_x, ntiles);
 }
 
 void launch_nms(const float* R, const MedianState* state, uint64_t* cand,
@@ -217,11 +237,11 @@ void launch_nms(const float* R, const MedianState* state, uint64_t* cand,
   const int tiles_y = (H + kNT_H - 1) / kNT_H;
   const int ntiles = tiles_x * tiles_y;
   switch (kh) {
-    case 0: launch_tile<0>(R, state, cand, cand_count, B, H, W, tiles_x, ntiles, mode, st); break;
-    case 1: launch_tile<1>(R, state, cand, cand_count, B, H, W, tiles_x, ntiles, mode, st); break;
-    case 2: launch_tile<2>(R, state, cand, cand_count, B, H, W, tiles_x, ntiles, mode, st); break;
-    case 3: launch_tile<3>(R, state, cand, cand_count, B, H, W, tiles_x, ntiles, mode, st); break;
-    case 4: launch_tile<4>(R, state, cand, cand_count, B, H, W, tiles_x, ntiles, mode, st); break;
+    case 0: launch_tile<0>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st); break;
+    case 1: launch_tile<1>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st); break;
+    case 2: launch_tile<2>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st); break;
+    case 3: launch_tile<3>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st); break;
+    case 4: launch_tile<4>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st); break;
     default: {
       dim3 grid(std::min(ntiles, kNmsBlocksPerPlane), B);
       hipLaunchKernelGGL(k_nms_generic<SFM_NMS_MAX_HALF>, grid, dim3(256), 0, st, R, state, cand, cand_count, H, W,

@@ -197,7 +197,7 @@ int reserve_impl(sfm_ctx* c, int B, int H, int W) {
   if ((rc = ensure(c, c->d_hist, (size_t)c->L * B * kMedBins1 * 4))) return rc;
   if ((rc = ensure(c, c->d_med, (size_t)c->L * B * sizeof(MedianState)))) return rc;
   if ((rc = ensure(c, c->d_medlist, (size_t)B * A0 * 4))) return rc;
-  if ((rc = ensure(c, c->d_counts, (size_t)3 * c->L * B * 8 * kCounterStride))) return rc;
+  if ((rc = ensure(c, c->d_counts, (size_t)4 * c->L * B * 8 * kCounterStride))) return rc;
   if ((rc = ensure(c, c->d_cand, (size_t)B * A0 * 8))) return rc;
   if ((rc = ensure(c, c->d_scratch, (size_t)B * A0 * 8))) return rc;
   size_t nk = (size_t)c->L * B * (size_t)std::max(c->kcap, 1);
@@ -233,10 +233,11 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     }
   }
   HIPCHK(c, hipMemsetAsync(c->d_hist.p, 0, (size_t)L * B * kMedBins1 * 4, st));
-  HIPCHK(c, hipMemsetAsync(c->d_counts.p, 0, (size_t)3 * L * B * 8 * kCounterStride, st));
+  HIPCHK(c, hipMemsetAsync(c->d_counts.p, 0, (size_t)4 * L * B * 8 * kCounterStride, st));
   unsigned long long* medcnt = as<unsigned long long>(c->d_counts);
   unsigned long long* candcnt = medcnt + (size_t)L * B * kCounterStride;    // certified NMS
   unsigned long long* candcnt2 = candcnt + (size_t)L * B * kCounterStride;  // fallback NMS
+  unsigned long long* donecnt = candcnt2 + (size_t)L * B * kCounterStride;  // Harris arrivals
   const float alpha = (float)c->p.alpha;  // NEP 50: the python float becomes float32
   // certified select: at least max(65536, 128 k) pixels at or above the threshold
   const int64_t vmin = std::max<int64_t>(65536, (int64_t)128 * c->kcap);
@@ -251,17 +252,14 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     kp.y = as<int32_t>(c->d_kpy) + ko;
     kp.conf = as<float>(c->d_kpc) + ko;
     kp.count = as<int32_t>(c->d_lc) + (size_t)l * B;
-    {
-      StageScope sc(c, SFM_PROF_HARRIS, st);
-      launch_harris(lvl[l], as<float>(c->d_R), hist, B, h, w, as<float>(c->d_gauss), c->p.gaussian_size,
-                    alpha, st);
-    }
     // levels too small to hold ~k window maxima above the median go straight to the exact
     // path (a size-only decision: no host synchronisation)
     const bool exact_level = c->exact_select || (int64_t)h * w < (int64_t)64 * c->kcap;
-    {
-      StageScope sc(c, SFM_PROF_MEDIAN, st);
-      launch_select_scan(hist, med, medcnt + co, B, h, w, vmin, exact_level ? 1 : 0, st);
+    {  // Harris + digit-1 histogram; its last workgroup per plane runs the select scan
+      StageScope sc(c, SFM_PROF_HARRIS, st);
+      const SelectScan scan{med, medcnt + co, donecnt + co, vmin, exact_level ? 1 : 0};
+      launch_harris(lvl[l], as<float>(c->d_R), hist, B, h, w, as<float>(c->d_gauss), c->p.gaussian_size,
+                    alpha, scan, st);
     }
     if (!exact_level) {  // certified planes (NaiveSIFT.py:77-120 without the exact median)
       {
