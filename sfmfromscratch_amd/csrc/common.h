@@ -176,6 +176,46 @@ SFM_DEV void bitonic_sort_u64(uint64_t* s, int P) {
   }
 }
 
+// One wavefront sorts N = 64 * E u64 keys held in registers, blocked layout (element m in
+// lane m / E, slot m % E), ascending.  Bitonic network with compile-time stages: strides
+// below E compare-exchange inside a lane, larger strides exchange with lane ^ (stride / E).
+template <int E>
+SFM_DEV void wave_bitonic_sort_u64(uint64_t (&k)[E]) {
+  const int lane = threadIdx.x & 63;
+  constexpr int N = 64 * E;
+#pragma unroll
+  for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride >= E) {
+        const int lm = stride / E;
+        const bool lower = (lane & lm) == 0;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          const bool asc = ((lane * E + r) & size) == 0;
+          const uint32_t olo = __shfl_xor((uint32_t)k[r], lm);
+          const uint32_t ohi = __shfl_xor((uint32_t)(k[r] >> 32), lm);
+          const uint64_t o = ((uint64_t)ohi << 32) | olo;
+          const bool take_min = (asc == lower);
+          const bool lt = o < k[r];
+          k[r] = (take_min == lt) ? o : k[r];
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          if ((r & stride) == 0) {
+            const bool asc = ((lane * E + r) & size) == 0;
+            const uint64_t a = k[r], b = k[r + stride];
+            const bool sw = (a > b) == asc;
+            k[r] = sw ? b : a;
+            k[r + stride] = sw ? a : b;
+          }
+        }
+      }
+    }
+  }
+}
+
 SFM_DEV int next_pow2(int v) {
   int p = 1;
   while (p < v) p <<= 1;

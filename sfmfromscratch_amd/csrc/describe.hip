@@ -49,6 +49,23 @@ __host__ __device__ inline DescLayout desc_layout(int fw, int rotate) {
   return L;
 }
 
+// Keys (fkey(ori[e]) << 32 | e, padding ~0) sorted by one wavefront in registers, then
+// written to s_keys in sorted order (16-B stores).
+template <int E>
+SFM_DEV void wave_sort_to_lds(const float* s_ori, int n, uint64_t* s_keys) {
+  const int lane = threadIdx.x & 63;
+  uint64_t k[E];
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const int e = lane * E + r;
+    k[r] = (e < n) ? (((uint64_t)fkey(s_ori[e]) << 32) | (uint32_t)e) : ~0ull;
+  }
+  wave_bitonic_sort_u64<E>(k);
+#pragma unroll
+  for (int r = 0; r < E; ++r) s_keys[lane * E + r] = k[r];
+  __syncthreads();
+}
+
 __global__ void __launch_bounds__(64) k_describe(const float* __restrict__ lvl, int H, int W, int fw,
                                                  int rotate, KpList kp, int kcap,
                                                  const int32_t* __restrict__ lc_all, int level, int B,
@@ -118,10 +135,21 @@ __global__ void __launch_bounds__(64) k_describe(const float* __restrict__ lvl, 
   // 3. dominant orientation (ScaleRotInvSIFT.py:24-31), 36 bins over the whole window
   double dom = 0.0;
   if (rotate) {
-    for (int e = lane; e < Ly.P; e += 64)
-      s_keys[e] = (e < n) ? (((uint64_t)fkey(s_ori[e]) << 32) | (uint32_t)e) : ~0ull;
-    __syncthreads();
-    bitonic_sort_u64(s_keys, Ly.P);
+    // sort (fkey(orientation), raster index): np.histogram's sort, made stable
+    if (Ly.P == 512) {
+      wave_sort_to_lds<8>(s_ori, n, s_keys);
+    } else if (Ly.P == 256) {
+      wave_sort_to_lds<4>(s_ori, n, s_keys);
+    } else if (Ly.P == 128) {
+      wave_sort_to_lds<2>(s_ori, n, s_keys);
+    } else if (Ly.P == 64) {
+      wave_sort_to_lds<1>(s_ori, n, s_keys);
+    } else {
+      for (int e = lane; e < Ly.P; e += 64)
+        s_keys[e] = (e < n) ? (((uint64_t)fkey(s_ori[e]) << 32) | (uint32_t)e) : ~0ull;
+      __syncthreads();
+      bitonic_sort_u64(s_keys, Ly.P);
+    }
     // weights in sorted order (parallel gather), zero-padded to a multiple of 4
     for (int m = lane; m < Ly.n4; m += 64) s_sw[m] = (m < n) ? s_mag[(uint32_t)s_keys[m]] : 0.0f;
     __syncthreads();
