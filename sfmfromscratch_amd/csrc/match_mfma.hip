@@ -65,7 +65,9 @@ __global__ void __launch_bounds__(256) k_match_prep(const float* __restrict__ de
   if (lane == 0) {
     float n2 = (float)s;
     float rn = (float)sqrt(s);
-    norm2[(int64_t)img * capP + row] = n2;
+    // padding rows: +inf squared norm, so their approximate distance is +inf and the
+    // sweep needs no bounds checks (never admitted, never in the top 2)
+    norm2[(int64_t)img * capP + row] = row < n ? n2 : INFINITY;
     rnorm[(int64_t)img * capP + row] = rn;
   }
 }
@@ -151,6 +153,7 @@ __global__ void __launch_bounds__(256) k_match_mfma(
   __shared__ __attribute__((aligned(16))) float sN[kTT2];
   __shared__ uint16_t sCand[kQB][kCandCap];
   __shared__ int sCnt[kQB];
+  __shared__ int sOff[kQB + 1];
   float* sDex = reinterpret_cast<float*>(&sT[0][0]);            // [kQB][kCandCap]
   float* sRed = sDex;                                            // [2][256] (after the re-rank)
   int* sRedJ = reinterpret_cast<int*>(sRed + 2 * 256);           // [256]
@@ -217,7 +220,6 @@ __global__ void __launch_bounds__(256) k_match_mfma(
     }
     const _Float16* tH = &sT[0][0];
     const _Float16* tL = &sT[1][0];
-    const bool full = st * kTT2 + kTT2 <= n2;  // uniform: only the last stage is partial
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       // 32 targets x 32 queries: hi.hi into ahh, hi.lo + lo.hi into ax (one chain each)
@@ -247,18 +249,12 @@ __global__ void __launch_bounds__(256) k_match_mfma(
                                  __builtin_fmaf(ahh[rr], -3.0517578125e-05f /* -2^-15 */, t2));
         }
       }
-      if (!full) {
-#pragma unroll
-        for (int rr = 0; rr < 16; ++rr) {
-          const int j = st * kTT2 + 32 * sub + (rr & 3) + 8 * (rr >> 2) + 4 * half;
-          d[rr] = j < n2 ? d[rr] : INFINITY;
-        }
-      }
-      // running top-2 (b1 <= b2): b2 = med3(b1, b2, d), b1 = min(b1, d)
+      // (targets past n2 are padding rows with norm2 = +inf: d = +inf)
+      // running top-2 (b1 <= b2): b2 = med3(b1, b2, d), b1 = med3(b1, d, -inf) = min
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
         b2 = __builtin_amdgcn_fmed3f(b1, b2, d[rr]);
-        b1 = fminf(b1, d[rr]);
+        b1 = __builtin_amdgcn_fmed3f(b1, d[rr], -INFINITY);
       }
       // the row's threshold (both halves merged), then admission
       const float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
@@ -283,17 +279,38 @@ __global__ void __launch_bounds__(256) k_match_mfma(
   }
   __syncthreads();  // sweep done: the stage buffers become the re-rank scratch
 
-  // exact re-rank of the collected candidates
-  int maxc = 0;
-  for (int i = 0; i < kQB; ++i) maxc = max(maxc, min(sCnt[i], kCandCap));
+  // exact re-rank of the collected candidates, flattened over the workgroup: row rl owns
+  // entries [sOff[rl], sOff[rl+1]) of the candidate list, every thread takes every 256th
+  if (tid < kQB) {
+    const int c = sCnt[tid];
+    sOff[tid + 1] = (c <= kCandCap && row0 + tid < n1) ? c : 0;
+  }
+  if (tid == 0) sOff[0] = 0;
+  __syncthreads();
+  if (tid < 64) {  // inclusive scan of the 128 counts by one wave (2 per lane)
+    int a = sOff[2 * tid + 1], b = sOff[2 * tid + 2];
+    int x = a + b;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off);
+      if (tid >= off) x += y;
+    }
+    sOff[2 * tid + 1] = x - b;
+    sOff[2 * tid + 2] = x;
+  }
+  __syncthreads();
+  const int total = sOff[kQB];
   const float* A = desc + (int64_t)i1 * cap * 128;
   const float* Bd = desc + (int64_t)i2 * cap * 128;
-  for (int idx = tid; idx < kQB * maxc; idx += 256) {
-    const int rl = idx % kQB, slot = idx / kQB;
-    const int c = sCnt[rl];
-    if (slot < c && c <= kCandCap && row0 + rl < n1)
-      sDex[rl * kCandCap + slot] =
-          exact_sqdist(A + (int64_t)(row0 + rl) * 128, Bd + (int64_t)sCand[rl][slot] * 128);
+  for (int e = tid; e < total; e += 256) {
+    int lo = 0, hi = kQB;  // the row with sOff[row] <= e < sOff[row + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (sOff[mid] <= e) lo = mid; else hi = mid;
+    }
+    const int rl = lo, slot = e - sOff[rl];
+    sDex[rl * kCandCap + slot] =
+        exact_sqdist(A + (int64_t)(row0 + rl) * 128, Bd + (int64_t)sCand[rl][slot] * 128);
   }
   __syncthreads();
   if (tid < kQB && row0 + tid < n1 && sCnt[tid] <= kCandCap) {
