@@ -16,6 +16,8 @@
 //      order (8 accumulators) and take (distance, index) minima -> ratio test.
 // Rows whose window overflows the per-row candidate list are recomputed exactly over
 // all targets (rare: only for runs of near-identical target descriptors).
+#include <stdlib.h>
+
 #include "kernels.h"
 
 namespace sfm {
@@ -123,6 +125,12 @@ SFM_DEV float exact_sqdist(const float* __restrict__ a, const float* __restrict_
   return u0 + u1;
 }
 
+// d~ rounded DOWN to bf16 (kept as its top 16 bits): truncation for positive values;
+// negative values (|d~| within E of 0) become -inf, which always passes the filter
+SFM_DEV uint16_t bf16_down(float v) {
+  return v >= 0.0f ? (uint16_t)(__float_as_uint(v) >> 16) : (uint16_t)0xFF80u;
+}
+
 SFM_DEV void top2_merge(float& b1, int& j1, float& b2, float ob1, int oj1, float ob2) {
   if (ob1 < b1 || (ob1 == b1 && oj1 < j1)) {
     b2 = fminf(b1, ob2);
@@ -143,27 +151,37 @@ static_assert(kCandCap <= 64, "admission masks are 64-bit at most");
 // gives a threshold thr = b2~ + 2E that only shrinks, so every target inside the final
 // window (d~ <= b2~_final + 2E) is admitted when visited; the admitted targets are then
 // re-ranked with the reference's exact float32 distance.
+// ABL (timing builds only; results are wrong unless 0): 6 = no re-rank, 8 = no appends
+template <int ABL>
 __global__ void __launch_bounds__(256) k_match_mfma(
     const float* __restrict__ desc, const int32_t* __restrict__ count, int64_t cap, int64_t capP,
     const _Float16* __restrict__ hi, const _Float16* __restrict__ lo, const float* __restrict__ norm2,
     const float* __restrict__ rnorm, const unsigned int* __restrict__ imgmax,
-    const int32_t* __restrict__ pairs, float ratio, RowBest* __restrict__ rows_out, int max_rows) {
+    const int32_t* __restrict__ pairs, int P, float ratio, RowBest* __restrict__ rows_out, int max_rows) {
   // stage buffer [hi|lo][64][kRowH]; after the sweep the space holds the re-rank scratch
   __shared__ __attribute__((aligned(16))) _Float16 sT[2][kStageHalves];
   __shared__ __attribute__((aligned(16))) float sN[kTT2];
   __shared__ uint16_t sCand[kQB][kCandCap];
+  __shared__ uint16_t sCandD[kQB][kCandCap];  // d~ rounded down to bf16 (for the final filter)
   __shared__ int sCnt[kQB];
   __shared__ int sOff[kQB + 1];
+  __shared__ float sThr[kQB];
   float* sDex = reinterpret_cast<float*>(&sT[0][0]);            // [kQB][kCandCap]
   float* sRed = sDex;                                            // [2][256] (after the re-rank)
   int* sRedJ = reinterpret_cast<int*>(sRed + 2 * 256);           // [256]
   static_assert(sizeof(sT) >= (size_t)kQB * kCandCap * 4, "re-rank scratch fits");
 
-  const int p = blockIdx.y;
+  // XCD-aware mapping (workgroups b and b + 8 share an XCD and its L2): group g = b % 8
+  // takes the pairs p = g (mod 8), so all query blocks of a pair stream its target table
+  // through one L2
+  const int QB = (max_rows + kQB - 1) / kQB;
+  const int grp = blockIdx.x & 7, slot8 = blockIdx.x >> 3;
+  const int p = grp + 8 * (slot8 / QB);
+  if (p >= P) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
   const int n1 = count[i1], n2 = count[i2];
-  const int row0 = blockIdx.x * kQB;
+  const int row0 = (slot8 % QB) * kQB;
   if (row0 >= n1 || n2 < 1) return;
 
   // this lane's query row (column of the MFMA output) and its fragments, kept in registers
@@ -211,6 +229,7 @@ __global__ void __launch_bounds__(256) k_match_mfma(
   if (tid < kTT2) sN[tid] = nrm_t0;
 
   float b1 = INFINITY, b2 = INFINITY;
+  uint32_t admit_x = 0;  // ABL 8 only
   for (int st = 0; st < nst; ++st) {
     __syncthreads();  // stage st visible
     float nrm_next = 0.0f;
@@ -220,6 +239,7 @@ __global__ void __launch_bounds__(256) k_match_mfma(
     }
     const _Float16* tH = &sT[0][0];
     const _Float16* tL = &sT[1][0];
+    float d[2][16];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       // 32 targets x 32 queries: hi.hi into ahh, hi.lo + lo.hi into ax (one chain each)
@@ -236,7 +256,6 @@ __global__ void __launch_bounds__(256) k_match_mfma(
       }
       // d~ = na + nb - 2 a.b with a.b = (ahh + ax 2^-11) 2^-16: two fmas by exact powers
       // of two (each rounding is covered by E's 4e-6 (na + nb) term)
-      float d[16];
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const float4 nb4 = *reinterpret_cast<const float4*>(&sN[32 * sub + 8 * g4 + 4 * half]);
@@ -245,7 +264,7 @@ __global__ void __launch_bounds__(256) k_match_mfma(
         for (int e = 0; e < 4; ++e) {
           const int rr = 4 * g4 + e;
           const float t2 = na + nbv[e];
-          d[rr] = __builtin_fmaf(ax[rr], -1.4901161193847656e-08f /* -2^-26 */,
+          d[sub][rr] = __builtin_fmaf(ax[rr], -1.4901161193847656e-08f /* -2^-26 */,
                                  __builtin_fmaf(ahh[rr], -3.0517578125e-05f /* -2^-15 */, t2));
         }
       }
@@ -253,21 +272,36 @@ __global__ void __launch_bounds__(256) k_match_mfma(
       // running top-2 (b1 <= b2): b2 = med3(b1, b2, d), b1 = med3(b1, d, -inf) = min
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) {
-        b2 = __builtin_amdgcn_fmed3f(b1, b2, d[rr]);
-        b1 = __builtin_amdgcn_fmed3f(b1, d[rr], -INFINITY);
+        b2 = __builtin_amdgcn_fmed3f(b1, b2, d[sub][rr]);
+        b1 = __builtin_amdgcn_fmed3f(b1, d[sub][rr], -INFINITY);
       }
-      // the row's threshold (both halves merged), then admission
+    }
+    // once per stage (a branch inside the sub-tile loop would split the block and stop the
+    // compiler overlapping one sub-tile's MFMAs with the other's epilogue): the row's
+    // running threshold (both halves merged; b2 only decreases, so it stays conservative),
+    // then the appends
+    {
       const float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
       const float thr = fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + 2.0f * E;
-      uint32_t m = 0;
+      uint32_t mm = 0;
 #pragma unroll
-      for (int rr = 0; rr < 16; ++rr) m |= (d[rr] <= thr) ? (1u << rr) : 0u;
-      if (qi < n1 && m) {  // reserve this lane's slots with one LDS atomic, then fill them
-        int slot = atomicAdd(&sCnt[ql], __popc(m));
-        const int jbase = st * kTT2 + 32 * sub + 4 * half;
-        for (; m; m &= m - 1, ++slot) {
-          const int rr = __builtin_ctz(m);
-          if (slot < kCandCap) sCand[ql][slot] = (uint16_t)(jbase + (rr & 3) + 8 * (rr >> 2));
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) mm |= (d[sub][rr] <= thr) ? (1u << (16 * sub + rr)) : 0u;
+      if (ABL == 8) {
+        admit_x ^= mm;
+      } else if (qi < n1 && mm) {  // reserve this lane's slots with one LDS atomic, then fill them
+        int slot = atomicAdd(&sCnt[ql], __popc(mm));
+        for (; mm; mm &= mm - 1, ++slot) {
+          const int bit = __builtin_ctz(mm), rr = bit & 15;
+          const int j = st * kTT2 + 32 * (bit >> 4) + 4 * half + (rr & 3) + 8 * (rr >> 2);
+          float dv = d[0][0];  // d~ of this bit (select chain: no dynamic register indexing)
+#pragma unroll
+          for (int k = 1; k < 32; ++k) dv = (bit == k) ? d[k >> 4][k & 15] : dv;
+          if (slot < kCandCap) {
+            sCand[ql][slot] = (uint16_t)j;
+            sCandD[ql][slot] = bf16_down(dv);
+          }
         }
       }
     }
@@ -277,12 +311,29 @@ __global__ void __launch_bounds__(256) k_match_mfma(
       if (tid < kTT2) sN[tid] = nrm_next;
     }
   }
+  {  // the row's final threshold (both halves merged)
+    const float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
+    if (half == 0) sThr[ql] = fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + 2.0f * E;
+  }
   __syncthreads();  // sweep done: the stage buffers become the re-rank scratch
+  if (ABL == 8 && admit_x == 0x7fffffffu) rows_out[0].col = 1;  // defeats dead-code elimination
+  if (ABL != 0) return;
 
   // exact re-rank of the collected candidates, flattened over the workgroup: row rl owns
   // entries [sOff[rl], sOff[rl+1]) of the candidate list, every thread takes every 256th
+  // keep only the candidates inside the row's FINAL window (their stored d~ is rounded
+  // down, so no window member is dropped): the running threshold admitted ~3x more
   if (tid < kQB) {
-    const int c = sCnt[tid];
+    int c = sCnt[tid];
+    if (c <= kCandCap && row0 + tid < n1) {
+      const float t = sThr[tid];
+      int k = 0;
+      for (int s = 0; s < c; ++s) {
+        const uint16_t dd = sCandD[tid][s];
+        if (__uint_as_float((uint32_t)dd << 16) <= t) sCand[tid][k++] = sCand[tid][s];
+      }
+      sCnt[tid] = c = k;
+    }
     sOff[tid + 1] = (c <= kCandCap && row0 + tid < n1) ? c : 0;
   }
   if (tid == 0) sOff[0] = 0;
@@ -375,8 +426,21 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
                        const _Float16* hi, const _Float16* lo, const float* norm2, const float* rnorm,
                        const unsigned int* imgmax, const int32_t* pairs, int P, float ratio,
                        RowBest* rows, int max_rows, hipStream_t st) {
-  hipLaunchKernelGGL(k_match_mfma, dim3((max_rows + kQB - 1) / kQB, P), dim3(256), 0, st, desc, count, cap,
-                     capP, hi, lo, norm2, rnorm, imgmax, pairs, ratio, rows, max_rows);
+  static const int abl = [] {
+    const char* e = getenv("SFMFEAT_MATCH_ABL");  // diagnostics only (tools/bench_match.py)
+    return e ? atoi(e) : 0;
+  }();
+  const int qb = (max_rows + kQB - 1) / kQB;
+  const dim3 grid((unsigned)(8 * ((P + 7) / 8) * qb));
+  if (abl == 6)
+    hipLaunchKernelGGL(k_match_mfma<6>, grid, dim3(256), 0, st, desc, count, cap, capP, hi, lo, norm2, rnorm, imgmax,
+                       pairs, P, ratio, rows, max_rows);
+  else if (abl == 8)
+    hipLaunchKernelGGL(k_match_mfma<8>, grid, dim3(256), 0, st, desc, count, cap, capP, hi, lo, norm2, rnorm, imgmax,
+                       pairs, P, ratio, rows, max_rows);
+  else
+    hipLaunchKernelGGL(k_match_mfma<0>, grid, dim3(256), 0, st, desc, count, cap, capP, hi, lo, norm2, rnorm, imgmax,
+                       pairs, P, ratio, rows, max_rows);
 }
 
 }  // namespace sfm
