@@ -40,6 +40,10 @@ struct sfm_ctx {
   int device = 0;
   sfm_params p;
   hipStream_t stream = nullptr;
+  // extraction fork/join: keypoint selection + description of level l run on `aux` while
+  // the caller's stream computes Harris + NMS of level l + 1 (events ev[0..SFM_MAX_LEVELS])
+  hipStream_t aux = nullptr;
+  hipEvent_t ev[SFM_MAX_LEVELS + 2] = {};
   std::string err;
   int L = 1;
   int kcap = 0;       // per-level keypoint capacity = int(k / L) (ScaleRotInvSIFT.py:90)
@@ -193,12 +197,12 @@ int reserve_impl(sfm_ctx* c, int B, int H, int W) {
   int rc;
   if ((rc = ensure(c, c->d_img0, (size_t)B * A0 * 4))) return rc;
   if ((rc = ensure(c, c->d_lvl, (size_t)B * Arest * 4))) return rc;
-  if ((rc = ensure(c, c->d_R, (size_t)B * A0 * 4))) return rc;
+  if ((rc = ensure(c, c->d_R, (size_t)B * (A0 + Arest) * 4))) return rc;       // one R map per level
   if ((rc = ensure(c, c->d_hist, (size_t)c->L * B * kMedBins1 * 4))) return rc;
   if ((rc = ensure(c, c->d_med, (size_t)c->L * B * sizeof(MedianState)))) return rc;
   if ((rc = ensure(c, c->d_medlist, (size_t)B * A0 * 4))) return rc;
   if ((rc = ensure(c, c->d_counts, (size_t)4 * c->L * B * 8 * kCounterStride))) return rc;
-  if ((rc = ensure(c, c->d_cand, (size_t)B * A0 * 8))) return rc;
+  if ((rc = ensure(c, c->d_cand, (size_t)B * (A0 + Arest) * 8))) return rc;    // candidates per level
   if ((rc = ensure(c, c->d_scratch, (size_t)B * A0 * 8))) return rc;
   size_t nk = (size_t)c->L * B * (size_t)std::max(c->kcap, 1);
   if ((rc = ensure(c, c->d_kpx, nk * 4))) return rc;
@@ -241,9 +245,18 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   const float alpha = (float)c->p.alpha;  // NEP 50: the python float becomes float32
   // certified select: at least max(65536, 128 k) pixels at or above the threshold
   const int64_t vmin = std::max<int64_t>(65536, (int64_t)128 * c->kcap);
+  // fork: the aux stream starts after the pyramid and the counter resets
+  hipStream_t ax = c->aux;
+  HIPCHK(c, hipEventRecord(c->ev[L], st));
+  HIPCHK(c, hipStreamWaitEvent(ax, c->ev[L], 0));
+  const int rotate = c->p.mode == SFM_MODE_NAIVE ? 0 : 1;
+  int64_t plane_off = 0;  // element offset of level l's planes in the per-level R / candidates
   for (int l = 0; l < L; ++l) {
     const int h = lv[l].h, w = lv[l].w;
     const size_t co = (size_t)l * B * kCounterStride;
+    float* Rl = as<float>(c->d_R) + plane_off;
+    uint64_t* candl = as<uint64_t>(c->d_cand) + plane_off;
+    plane_off += (int64_t)B * h * w;
     uint32_t* hist = as<uint32_t>(c->d_hist) + (size_t)l * B * kMedBins1;
     MedianState* med = as<MedianState>(c->d_med) + (size_t)l * B;
     KpList kp;
@@ -255,47 +268,46 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     // levels too small to hold ~k window maxima above the median go straight to the exact
     // path (a size-only decision: no host synchronisation)
     const bool exact_level = c->exact_select || (int64_t)h * w < (int64_t)64 * c->kcap;
-    {  // Harris + digit-1 histogram; its last workgroup per plane runs the select scan
+    // caller's stream: Harris (+ fused select scan) and the certified NMS of level l
+    {
       StageScope sc(c, SFM_PROF_HARRIS, st);
       const SelectScan scan{med, medcnt + co, donecnt + co, vmin, exact_level ? 1 : 0};
-      launch_harris(lvl[l], as<float>(c->d_R), hist, B, h, w, as<float>(c->d_gauss), c->p.gaussian_size,
-                    alpha, scan, st);
+      launch_harris(lvl[l], Rl, hist, B, h, w, as<float>(c->d_gauss), c->p.gaussian_size, alpha, scan, st);
     }
-    if (!exact_level) {  // certified planes (NaiveSIFT.py:77-120 without the exact median)
-      {
-        StageScope sc(c, SFM_PROF_NMS, st);
-        launch_nms(as<float>(c->d_R), med, as<uint64_t>(c->d_cand), candcnt + co, B, h, w, c->p.ksize, 0, st);
-      }
-      StageScope sc(c, SFM_PROF_TOPK, st);
-      launch_topk(as<uint64_t>(c->d_cand), candcnt + co, as<uint64_t>(c->d_scratch), kp, std::max(c->kcap, 1),
-                  c->kcap, B, h, w, lv[l].fw / 2, med, 0, st);
-    }
-    // exact path for the planes flagged `fallback` (NaiveSIFT.py:77-120); no-ops otherwise
-    {
-      StageScope sc(c, SFM_PROF_MEDIAN, st);
-      launch_median_exact(as<float>(c->d_R), med, as<uint32_t>(c->d_medlist), medcnt + co, B, h, w, st);
-    }
-    {
+    if (!exact_level) {
       StageScope sc(c, SFM_PROF_NMS, st);
-      launch_nms(as<float>(c->d_R), med, as<uint64_t>(c->d_cand), candcnt2 + co, B, h, w, c->p.ksize, 1, st);
+      launch_nms(Rl, med, candl, candcnt + co, B, h, w, c->p.ksize, 0, st);
     }
-    StageScope sc(c, SFM_PROF_TOPK, st);
-    launch_topk(as<uint64_t>(c->d_cand), candcnt2 + co, as<uint64_t>(c->d_scratch), kp, std::max(c->kcap, 1),
-                c->kcap, B, h, w, lv[l].fw / 2, med, 1, st);
+    HIPCHK(c, hipEventRecord(c->ev[l], st));
+    // aux stream: top-k (certified planes), the exact path for the planes flagged
+    // `fallback` (no-ops otherwise), then the descriptors of level l
+    HIPCHK(c, hipStreamWaitEvent(ax, c->ev[l], 0));
+    if (!exact_level) {
+      StageScope sc(c, SFM_PROF_TOPK, ax);
+      launch_topk(candl, candcnt + co, as<uint64_t>(c->d_scratch), kp, std::max(c->kcap, 1), c->kcap, B, h, w,
+                  lv[l].fw / 2, med, 0, ax);
+    }
+    {
+      StageScope sc(c, SFM_PROF_MEDIAN, ax);
+      launch_median_exact(Rl, med, as<uint32_t>(c->d_medlist), medcnt + co, B, h, w, ax);
+    }
+    {
+      StageScope sc(c, SFM_PROF_NMS, ax);
+      launch_nms(Rl, med, candl, candcnt2 + co, B, h, w, c->p.ksize, 1, ax);
+    }
+    {
+      StageScope sc(c, SFM_PROF_TOPK, ax);
+      launch_topk(candl, candcnt2 + co, as<uint64_t>(c->d_scratch), kp, std::max(c->kcap, 1), c->kcap, B, h, w,
+                  lv[l].fw / 2, med, 1, ax);
+    }
+    StageScope sc(c, SFM_PROF_DESCRIBE, ax);
+    launch_describe(lvl[l], B, h, w, lv[l].fw, rotate, kp, c->kcap, as<int32_t>(c->d_lc), l, L, lv[l].scale, xy,
+                    desc, conf, cap, ax);
   }
-  const int rotate = c->p.mode == SFM_MODE_NAIVE ? 0 : 1;
-  for (int l = 0; l < L; ++l) {
-    KpList kp;
-    size_t ko = (size_t)l * B * std::max(c->kcap, 1);
-    kp.x = as<int32_t>(c->d_kpx) + ko;
-    kp.y = as<int32_t>(c->d_kpy) + ko;
-    kp.conf = as<float>(c->d_kpc) + ko;
-    kp.count = as<int32_t>(c->d_lc) + (size_t)l * B;
-    StageScope sc(c, SFM_PROF_DESCRIBE, st);
-    launch_describe(lvl[l], B, lv[l].h, lv[l].w, lv[l].fw, rotate, kp, c->kcap, as<int32_t>(c->d_lc), l,
-                    L, lv[l].scale, xy, desc, conf, cap, st);
-  }
-  launch_finalize_counts(as<int32_t>(c->d_lc), B, L, count, st);
+  launch_finalize_counts(as<int32_t>(c->d_lc), B, L, count, ax);
+  // join: the caller's stream waits for the aux work
+  HIPCHK(c, hipEventRecord(c->ev[L + 1], ax));
+  HIPCHK(c, hipStreamWaitEvent(st, c->ev[L + 1], 0));
   HIPCHK(c, hipGetLastError());
   return SFM_OK;
 }
@@ -422,13 +434,23 @@ int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out) {
   int gs = p->gaussian_size;
   if (p->gauss_kernel_set) memcpy(c->gauss, p->gauss_kernel, sizeof(float) * gs * gs);
   else gaussian_taps(gs, p->sigma, c->gauss);
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  bool ok = hipSetDevice(device) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess;
+  for (hipEvent_t& e : c->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
+    for (hipEvent_t e : c->ev)
+      if (e) (void)hipEventDestroy(e);
     delete c;
     return SFM_EDEVICE;
   }
   if (ensure(c, c->d_gauss, sizeof(float) * gs * gs) ||
       hipMemcpy(c->d_gauss.p, c->gauss, sizeof(float) * gs * gs, hipMemcpyHostToDevice) != hipSuccess) {
     (void)hipStreamDestroy(c->stream);
+    (void)hipStreamDestroy(c->aux);
+    for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
     delete c;
     return SFM_EDEVICE;
   }
@@ -455,6 +477,9 @@ int32_t sfm_ctx_destroy(sfm_ctx* c) {
   }
   for (hipEvent_t e : c->prof_pool) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->aux) (void)hipStreamDestroy(c->aux);
+  for (hipEvent_t e : c->ev)
+    if (e) (void)hipEventDestroy(e);
   delete c;
   return SFM_OK;
 }
