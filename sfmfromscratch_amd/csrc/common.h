@@ -104,25 +104,33 @@ SFM_DEV int64_t block_append(unsigned long long* counter, uint32_t cnt, uint32_t
   return r;
 }
 
-// Block-wide: given a histogram of `nb` bins in LDS (nb a multiple of blockDim.x), find
-// the bin holding 0-based rank `rank`; s_out = {bin, count before bin}.  s_scan holds
-// blockDim.x uint32.  Every thread of the block must call it.
+// Inclusive prefix sum of one uint32 per lane across the wavefront (shuffles, no LDS).
+SFM_DEV uint32_t wave_inclusive_scan(uint32_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  return x;
+}
+
+// Block-wide: given a histogram of `nb` bins in LDS (nb a multiple of blockDim.x, blockDim.x
+// a multiple of 64), find the bin holding 0-based rank `rank`; s_out = {bin, count before
+// bin}.  s_scan holds >= blockDim.x / 64 uint32 (wave totals).  Every thread calls it.
+// Wave-shuffle scan: two block barriers.
 SFM_DEV void find_bin(const uint32_t* s_h, int nb, uint32_t rank, uint32_t* s_scan,
                       uint32_t* s_out) {
-  const int tid = threadIdx.x, nt = blockDim.x;
+  const int tid = threadIdx.x, nt = blockDim.x, wid = tid >> 6;
   const int per = nb / nt;
   uint32_t local = 0;
   for (int i = 0; i < per; ++i) local += s_h[tid * per + i];
-  s_scan[tid] = local;
+  const uint32_t x = wave_inclusive_scan(local);
+  if ((tid & 63) == 63) s_scan[wid] = x;
   __syncthreads();
-  for (int off = 1; off < nt; off <<= 1) {
-    uint32_t v = (tid >= off) ? s_scan[tid - off] : 0u;
-    __syncthreads();
-    s_scan[tid] += v;
-    __syncthreads();
-  }
-  uint32_t incl = s_scan[tid];
-  uint32_t excl = incl - local;
+  uint32_t base = 0;
+  for (int w = 0; w < wid; ++w) base += s_scan[w];
+  const uint32_t excl = base + x - local, incl = excl + local;
   if (rank >= excl && rank < incl) {
     uint32_t c = excl;
     for (int i = 0; i < per; ++i) {
@@ -139,28 +147,33 @@ SFM_DEV void find_bin(const uint32_t* s_h, int nb, uint32_t rank, uint32_t* s_sc
 }
 
 // Block-wide exclusive scan of one uint32 per thread; returns the exclusive prefix and
-// writes the block total to *total.  s_scan holds blockDim.x uint32.
+// writes the block total to *total.  s_scan holds >= blockDim.x / 64 + 1 uint32.
 SFM_DEV uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_scan, uint32_t* total) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-  s_scan[tid] = v;
+  const int tid = threadIdx.x, nt = blockDim.x, wid = tid >> 6, nw = nt >> 6;
+  const uint32_t x = wave_inclusive_scan(v);
+  if ((tid & 63) == 63) s_scan[wid] = x;
   __syncthreads();
-  for (int off = 1; off < nt; off <<= 1) {
-    uint32_t t = (tid >= off) ? s_scan[tid - off] : 0u;
-    __syncthreads();
-    s_scan[tid] += t;
-    __syncthreads();
+  uint32_t base = 0, all = 0;
+  for (int w = 0; w < nw; ++w) {
+    const uint32_t t = s_scan[w];
+    base += w < wid ? t : 0u;
+    all += t;
   }
-  uint32_t incl = s_scan[tid];
-  *total = s_scan[nt - 1];
+  *total = all;
   __syncthreads();
-  return incl - v;
+  return base + x - v;
 }
 
-// Block-wide ascending bitonic sort of P (power of two) uint64 keys in LDS.
+// Block-wide ascending bitonic sort of P (power of two) uint64 keys in LDS (blockDim.x a
+// multiple of 64).  Stages with stride < 64 stay inside an aligned 128-key chunk that one
+// wave owns (pair i of chunk i / 64), so they need only wave-level ordering; the larger
+// strides are separated by block barriers.
 SFM_DEV void bitonic_sort_u64(uint64_t* s, int P) {
   const int tid = threadIdx.x, nt = blockDim.x;
   for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const bool wide = stride >= 64;
+      if (wide) __syncthreads();
       for (int i = tid; i < (P >> 1); i += nt) {
         int pos = 2 * i - (i & (stride - 1));
         int partner = pos + stride;
@@ -171,9 +184,16 @@ SFM_DEV void bitonic_sort_u64(uint64_t* s, int P) {
           s[partner] = a;
         }
       }
-      __syncthreads();
+      if (wide) {
+        __syncthreads();
+      } else {  // LDS ops of one wave are processed in order; keep the compiler from reordering
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
     }
   }
+  __syncthreads();
 }
 
 // One wavefront sorts N = 64 * E u64 keys held in registers, blocked layout (element m in
