@@ -43,7 +43,7 @@ struct sfm_ctx {
   // extraction fork/join: keypoint selection + description of level l run on `aux` while
   // the caller's stream computes Harris + NMS of level l + 1 (events ev[0..SFM_MAX_LEVELS])
   hipStream_t aux = nullptr;
-  hipEvent_t ev[SFM_MAX_LEVELS + 2] = {};
+  hipEvent_t ev[SFM_MAX_LEVELS + 3] = {};
   std::string err;
   int L = 1;
   int kcap = 0;       // per-level keypoint capacity = int(k / L) (ScaleRotInvSIFT.py:90)
@@ -200,10 +200,10 @@ int reserve_impl(sfm_ctx* c, int B, int H, int W) {
   if ((rc = ensure(c, c->d_R, (size_t)B * (A0 + Arest) * 4))) return rc;       // one R map per level
   if ((rc = ensure(c, c->d_hist, (size_t)c->L * B * kMedBins1 * 4))) return rc;
   if ((rc = ensure(c, c->d_med, (size_t)c->L * B * sizeof(MedianState)))) return rc;
-  if ((rc = ensure(c, c->d_medlist, (size_t)B * A0 * 4))) return rc;
+  if ((rc = ensure(c, c->d_medlist, (size_t)2 * B * A0 * 4))) return rc;     // aux | main stream
   if ((rc = ensure(c, c->d_counts, (size_t)4 * c->L * B * 8 * kCounterStride))) return rc;
   if ((rc = ensure(c, c->d_cand, (size_t)B * (A0 + Arest) * 8))) return rc;    // candidates per level
-  if ((rc = ensure(c, c->d_scratch, (size_t)B * A0 * 8))) return rc;
+  if ((rc = ensure(c, c->d_scratch, (size_t)2 * B * A0 * 8))) return rc;     // aux | main stream
   size_t nk = (size_t)c->L * B * (size_t)std::max(c->kcap, 1);
   if ((rc = ensure(c, c->d_kpx, nk * 4))) return rc;
   if ((rc = ensure(c, c->d_kpy, nk * 4))) return rc;
@@ -245,69 +245,98 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   const float alpha = (float)c->p.alpha;  // NEP 50: the python float becomes float32
   // certified select: at least max(65536, 128 k) pixels at or above the threshold
   const int64_t vmin = std::max<int64_t>(65536, (int64_t)128 * c->kcap);
-  // fork: the aux stream starts after the pyramid and the counter resets
+  // Fork/join over two streams.  The caller's stream runs Harris (+ fused select scan) and
+  // the certified NMS of every level; the keypoint selection (top-k, the exact path for
+  // the planes flagged `fallback`) and the descriptors of the two largest levels run on
+  // `aux`, overlapping the later levels' Harris; the small levels' selection and
+  // descriptors run on the caller's stream once its Harris work is done.  Descriptors of
+  // level l need the keypoint counts of levels < l (slot offsets): ev[L + 2 + l].
   hipStream_t ax = c->aux;
+  const int L_aux = std::min(L, 2);
   HIPCHK(c, hipEventRecord(c->ev[L], st));
   HIPCHK(c, hipStreamWaitEvent(ax, c->ev[L], 0));
   const int rotate = c->p.mode == SFM_MODE_NAIVE ? 0 : 1;
+  struct LevelBufs {
+    float* R;
+    uint64_t* cand;
+    MedianState* med;
+    KpList kp;
+    size_t co;
+    bool exact;
+  };
+  std::vector<LevelBufs> lb(L);
   int64_t plane_off = 0;  // element offset of level l's planes in the per-level R / candidates
   for (int l = 0; l < L; ++l) {
     const int h = lv[l].h, w = lv[l].w;
-    const size_t co = (size_t)l * B * kCounterStride;
-    float* Rl = as<float>(c->d_R) + plane_off;
-    uint64_t* candl = as<uint64_t>(c->d_cand) + plane_off;
+    LevelBufs& e = lb[l];
+    e.co = (size_t)l * B * kCounterStride;
+    e.R = as<float>(c->d_R) + plane_off;
+    e.cand = as<uint64_t>(c->d_cand) + plane_off;
     plane_off += (int64_t)B * h * w;
-    uint32_t* hist = as<uint32_t>(c->d_hist) + (size_t)l * B * kMedBins1;
-    MedianState* med = as<MedianState>(c->d_med) + (size_t)l * B;
-    KpList kp;
-    size_t ko = (size_t)l * B * std::max(c->kcap, 1);
-    kp.x = as<int32_t>(c->d_kpx) + ko;
-    kp.y = as<int32_t>(c->d_kpy) + ko;
-    kp.conf = as<float>(c->d_kpc) + ko;
-    kp.count = as<int32_t>(c->d_lc) + (size_t)l * B;
+    e.med = as<MedianState>(c->d_med) + (size_t)l * B;
+    const size_t ko = (size_t)l * B * std::max(c->kcap, 1);
+    e.kp.x = as<int32_t>(c->d_kpx) + ko;
+    e.kp.y = as<int32_t>(c->d_kpy) + ko;
+    e.kp.conf = as<float>(c->d_kpc) + ko;
+    e.kp.count = as<int32_t>(c->d_lc) + (size_t)l * B;
     // levels too small to hold ~k window maxima above the median go straight to the exact
     // path (a size-only decision: no host synchronisation)
-    const bool exact_level = c->exact_select || (int64_t)h * w < (int64_t)64 * c->kcap;
-    // caller's stream: Harris (+ fused select scan) and the certified NMS of level l
+    e.exact = c->exact_select || (int64_t)h * w < (int64_t)64 * c->kcap;
+  }
+  auto select_level = [&](int l, hipStream_t s) {  // top-k + exact fallback of level l
+    const LevelBufs& e = lb[l];
+    const int h = lv[l].h, w = lv[l].w;
+    if (!e.exact) {
+      StageScope sc(c, SFM_PROF_TOPK, s);
+      launch_topk(e.cand, candcnt + e.co, as<uint64_t>(c->d_scratch), e.kp, std::max(c->kcap, 1), c->kcap, B, h, w,
+                  lv[l].fw / 2, e.med, 0, s);
+    }
+    {
+      StageScope sc(c, SFM_PROF_MEDIAN, s);
+      launch_median_exact(e.R, e.med, as<uint32_t>(c->d_medlist) + (l < L_aux ? 0 : (int64_t)B * H * W), medcnt + e.co,
+                          B, h, w, s);
+    }
+    {
+      StageScope sc(c, SFM_PROF_NMS, s);
+      launch_nms(e.R, e.med, e.cand, candcnt2 + e.co, B, h, w, c->p.ksize, 1, s);
+    }
+    StageScope sc(c, SFM_PROF_TOPK, s);
+    launch_topk(e.cand, candcnt2 + e.co, as<uint64_t>(c->d_scratch) + (l < L_aux ? 0 : (int64_t)B * H * W), e.kp,
+                std::max(c->kcap, 1), c->kcap, B, h, w, lv[l].fw / 2, e.med, 1, s);
+  };
+  auto describe_level = [&](int l, hipStream_t s) {
+    StageScope sc(c, SFM_PROF_DESCRIBE, s);
+    launch_describe(lvl[l], B, lv[l].h, lv[l].w, lv[l].fw, rotate, lb[l].kp, c->kcap, as<int32_t>(c->d_lc), l, L,
+                    lv[l].scale, xy, desc, conf, cap, s);
+  };
+  for (int l = 0; l < L; ++l) {
+    const LevelBufs& e = lb[l];
+    const int h = lv[l].h, w = lv[l].w;
+    uint32_t* hist = as<uint32_t>(c->d_hist) + (size_t)l * B * kMedBins1;
     {
       StageScope sc(c, SFM_PROF_HARRIS, st);
-      const SelectScan scan{med, medcnt + co, donecnt + co, vmin, exact_level ? 1 : 0};
-      launch_harris(lvl[l], Rl, hist, B, h, w, as<float>(c->d_gauss), c->p.gaussian_size, alpha, scan, st);
+      const SelectScan scan{e.med, medcnt + e.co, donecnt + e.co, vmin, e.exact ? 1 : 0};
+      launch_harris(lvl[l], e.R, hist, B, h, w, as<float>(c->d_gauss), c->p.gaussian_size, alpha, scan, st);
     }
-    if (!exact_level) {
+    if (!e.exact) {
       StageScope sc(c, SFM_PROF_NMS, st);
-      launch_nms(Rl, med, candl, candcnt + co, B, h, w, c->p.ksize, 0, st);
+      launch_nms(e.R, e.med, e.cand, candcnt + e.co, B, h, w, c->p.ksize, 0, st);
     }
-    HIPCHK(c, hipEventRecord(c->ev[l], st));
-    // aux stream: top-k (certified planes), the exact path for the planes flagged
-    // `fallback` (no-ops otherwise), then the descriptors of level l
-    HIPCHK(c, hipStreamWaitEvent(ax, c->ev[l], 0));
-    if (!exact_level) {
-      StageScope sc(c, SFM_PROF_TOPK, ax);
-      launch_topk(candl, candcnt + co, as<uint64_t>(c->d_scratch), kp, std::max(c->kcap, 1), c->kcap, B, h, w,
-                  lv[l].fw / 2, med, 0, ax);
+    if (l < L_aux) {
+      HIPCHK(c, hipEventRecord(c->ev[l], st));
+      HIPCHK(c, hipStreamWaitEvent(ax, c->ev[l], 0));
+      select_level(l, ax);
+      if (l == L_aux - 1) HIPCHK(c, hipEventRecord(c->ev[L + 2], ax));  // counts of the aux levels known
+      describe_level(l, ax);
     }
-    {
-      StageScope sc(c, SFM_PROF_MEDIAN, ax);
-      launch_median_exact(Rl, med, as<uint32_t>(c->d_medlist), medcnt + co, B, h, w, ax);
-    }
-    {
-      StageScope sc(c, SFM_PROF_NMS, ax);
-      launch_nms(Rl, med, candl, candcnt2 + co, B, h, w, c->p.ksize, 1, ax);
-    }
-    {
-      StageScope sc(c, SFM_PROF_TOPK, ax);
-      launch_topk(candl, candcnt2 + co, as<uint64_t>(c->d_scratch), kp, std::max(c->kcap, 1), c->kcap, B, h, w,
-                  lv[l].fw / 2, med, 1, ax);
-    }
-    StageScope sc(c, SFM_PROF_DESCRIBE, ax);
-    launch_describe(lvl[l], B, h, w, lv[l].fw, rotate, kp, c->kcap, as<int32_t>(c->d_lc), l, L, lv[l].scale, xy,
-                    desc, conf, cap, ax);
   }
-  launch_finalize_counts(as<int32_t>(c->d_lc), B, L, count, ax);
+  for (int l = L_aux; l < L; ++l) select_level(l, st);
+  if (L > L_aux) HIPCHK(c, hipStreamWaitEvent(st, c->ev[L + 2], 0));
+  for (int l = L_aux; l < L; ++l) describe_level(l, st);
   // join: the caller's stream waits for the aux work
   HIPCHK(c, hipEventRecord(c->ev[L + 1], ax));
   HIPCHK(c, hipStreamWaitEvent(st, c->ev[L + 1], 0));
+  launch_finalize_counts(as<int32_t>(c->d_lc), B, L, count, st);
   HIPCHK(c, hipGetLastError());
   return SFM_OK;
 }
