@@ -9,6 +9,8 @@
 // fixed-order norm of DESIGN.md §Numerics.
 #include "kernels.h"
 
+#include <stdlib.h>
+
 namespace sfm {
 
 // numpy.linspace(-pi, pi, num)[i]: i*step + start, last element = stop exactly.
@@ -313,6 +315,13 @@ void launch_describe(const float* lvl, int B, int H, int W, int fw, int rotate, 
                      hipStream_t st) {
   (void)L;
   if (kcap <= 0) return;
+  static const bool one_per_wave = [] {
+    const char* v = getenv("SFMFEAT_DESCRIBE");
+    return v && v[0] == 'w';  // "wave": the one-keypoint-per-wavefront kernel (A/B timing)
+  }();
+  if (!one_per_wave && launch_describe_quad(lvl, B, H, W, fw, rotate, kp, kcap, level_counts_all, level,
+                                            scale, out_xy, out_desc, out_conf, out_cap, st))
+    return;
   size_t lds = describe_lds_bytes(fw, rotate);
   hipLaunchKernelGGL(k_describe, dim3(kcap, B), dim3(64), lds, st, lvl, H, W, fw, rotate, kp, kcap,
                      level_counts_all, level, B, scale, out_xy, out_desc, out_conf, out_cap);

@@ -165,6 +165,10 @@ void launch_topk(const uint64_t* cand, const unsigned long long* cand_count, uin
                  KpList kp, int kcap, int k, int B, int H, int W, int half_window,
                  MedianState* state, int mode, hipStream_t st);
 
+// describe_q.hip: four keypoints per wavefront for window widths 2..22 (false: not handled)
+bool launch_describe_quad(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp, int kcap,
+                          const int32_t* level_counts_all, int level, double scale, int32_t* out_xy,
+                          float* out_desc, float* out_conf, int64_t out_cap, hipStream_t st);
 // describe.hip: descriptors of one level written into the output slot table.
 void launch_describe(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp,
                      int kcap, const int32_t* level_counts_all, int level, int L, double scale,
