@@ -183,6 +183,9 @@ int32_t sfm_match_pairs_dev(sfm_ctx* ctx, const float* desc, const int32_t* coun
 #define SFM_PROF_MATCH_POST 8
 #define SFM_PROF_STAGES 9
 int32_t sfm_profile_enable(sfm_ctx* ctx, int32_t on);
+/* Bracket only the stages whose bit (1 << SFM_PROF_*) is set in `mask` (0 = off): the
+ * bench times its headline run with the dominant stage's events alone. */
+int32_t sfm_profile_stages(sfm_ctx* ctx, int32_t mask);
 int32_t sfm_profile_read(sfm_ctx* ctx, double* ms, int64_t* launches, int32_t reset);
 
 /* ---------------- diagnostics (used by the parity tests) ----------------

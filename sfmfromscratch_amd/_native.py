@@ -48,6 +48,7 @@ SIGNATURES = {
     "sfm_match_pairs_dev": (ctypes.c_int32, [_vp, _vp, _vp, ctypes.c_int32, ctypes.c_int64, _vp, ctypes.c_int32,
                                              ctypes.c_float, _vp, _vp, _vp, _vp]),
     "sfm_profile_enable": (ctypes.c_int32, [_vp, ctypes.c_int32]),
+    "sfm_profile_stages": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "sfm_profile_read": (ctypes.c_int32, [_vp, ctypes.POINTER(ctypes.c_double), _i64p, ctypes.c_int32]),
     "sfm_debug_time_harris": (ctypes.c_float, [ctypes.c_int32] * 6),
     "sfm_debug_select_stats": (ctypes.c_int32, [_vp, _i32p, _i32p]),
@@ -212,6 +213,13 @@ class Context:
 
     def profile_enable(self, on: bool = True):
         check(self.lib.sfm_profile_enable(self.handle, 1 if on else 0), self.handle)
+
+    def profile_stages(self, names):
+        """Bracket only the named stages (PROF_STAGES) with events; [] turns profiling off."""
+        mask = 0
+        for k in names:
+            mask |= 1 << self.PROF_STAGES.index(k)
+        check(self.lib.sfm_profile_stages(self.handle, mask), self.handle)
 
     def profile_read(self, reset: bool = True) -> dict:
         ms = np.zeros(len(self.PROF_STAGES), np.float64)

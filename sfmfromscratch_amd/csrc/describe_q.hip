@@ -20,6 +20,8 @@
 //   one-keypoint kernel, normalise, sqrt.
 #include "kernels.h"
 
+#include <stdlib.h>
+
 namespace sfm {
 namespace dq {
 
@@ -83,25 +85,34 @@ SFM_DEV uint32_t rxor(uint32_t v) {
 template <int X>
 SFM_DEV float rxorf(float v) { return __uint_as_float(rxor<X>(__float_as_uint(v))); }
 template <int X>
-SFM_DEV uint64_t rxor64(uint64_t v) {
-  return ((uint64_t)rxor<X>((uint32_t)(v >> 32)) << 32) | rxor<X>((uint32_t)v);
+SFM_DEV double rxord(double v) {
+  const uint64_t u = __double_as_longlong(v);
+  return __longlong_as_double((long long)(((uint64_t)rxor<X>((uint32_t)(u >> 32)) << 32) | rxor<X>((uint32_t)u)));
 }
 
-SFM_DEV void cas_up(uint64_t& a, uint64_t& b) {
-  const bool sw = a > b;
-  const uint64_t t = a;
-  a = sw ? b : a;
-  b = sw ? t : b;
+// Sort keys as doubles: kBias + (fkey << 9 | pixel) is a positive normal double for every
+// 41-bit payload, so the double order is the payload order and a compare-exchange is one
+// v_min_f64 + one v_max_f64 (no lane masks; the file is built with -fno-honor-nans so
+// they are not preceded by canonicalisations).  kPad sorts after every key.
+constexpr uint64_t kBias = 1ull << 52;
+constexpr uint64_t kPad = kBias + (1ull << 41);
+SFM_DEV double dkey(uint64_t payload) { return __longlong_as_double((long long)(kBias + payload)); }
+SFM_DEV uint64_t dpayload(double k) { return (uint64_t)__double_as_longlong(k) - kBias; }
+
+SFM_DEV void cas_up(double& a, double& b) {
+  const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
+  a = lo;
+  b = hi;
 }
-SFM_DEV uint64_t keep_or_take(bool lower, uint64_t mine, uint64_t other) {
-  const bool take = lower ? (other < mine) : (other > mine);
-  return take ? other : mine;
+SFM_DEV double keep_or_take(bool lower, double mine, double other) {
+  const double lo = __builtin_fmin(mine, other), hi = __builtin_fmax(mine, other);
+  return lower ? lo : hi;
 }
 
 // Bitonic sort (all comparators ascending: each merge starts with the mirrored compare)
 // of 16*E keys held as lane gl, register r <-> position gl*E + r of one 16-lane row.
 template <int E, int S>
-SFM_DEV void half_clean(uint64_t (&k)[E], int gl) {
+SFM_DEV void half_clean(double (&k)[E], int gl) {
   if constexpr (S >= 1) {
     if constexpr (S < E) {
 #pragma unroll
@@ -111,13 +122,13 @@ SFM_DEV void half_clean(uint64_t (&k)[E], int gl) {
       constexpr int X = S / E;
       const bool lower = (gl & X) == 0;
 #pragma unroll
-      for (int r = 0; r < E; ++r) k[r] = keep_or_take(lower, k[r], rxor64<X>(k[r]));
+      for (int r = 0; r < E; ++r) k[r] = keep_or_take(lower, k[r], rxord<X>(k[r]));
     }
     half_clean<E, S / 2>(k, gl);
   }
 }
 template <int E, int SIZE>
-SFM_DEV void merge_level(uint64_t (&k)[E], int gl) {
+SFM_DEV void merge_level(double (&k)[E], int gl) {
   if constexpr (SIZE <= 16 * E) {
     if constexpr (SIZE <= E) {
 #pragma unroll
@@ -127,12 +138,12 @@ SFM_DEV void merge_level(uint64_t (&k)[E], int gl) {
       constexpr int X = SIZE / E - 1;
       const bool lower = (gl & ((X + 1) >> 1)) == 0;
       if constexpr (E == 1) {
-        k[0] = keep_or_take(lower, k[0], rxor64<X>(k[0]));
+        k[0] = keep_or_take(lower, k[0], rxord<X>(k[0]));
       } else {
 #pragma unroll
         for (int r = 0; r < E / 2; ++r) {
-          const uint64_t oa = rxor64<X>(k[E - 1 - r]);
-          const uint64_t ob = rxor64<X>(k[r]);
+          const double oa = rxord<X>(k[E - 1 - r]);
+          const double ob = rxord<X>(k[r]);
           k[r] = keep_or_take(lower, k[r], oa);
           k[E - 1 - r] = keep_or_take(lower, k[E - 1 - r], ob);
         }
@@ -169,6 +180,12 @@ SFM_DEV void grad_at(const float* c, int pw, float& mag, float& ori) {
   ori = svml_atan2f(gy, gx);
 }
 
+SFM_DEV void cas_up(uint32_t& a, uint32_t& b) {
+  const uint32_t lo = min(a, b), hi = max(a, b);
+  a = lo;
+  b = hi;
+}
+
 // Batcher odd-even merge network over 16 register slots (ascending).
 template <typename T>
 SFM_DEV void batcher16(T (&q)[16]) {
@@ -181,16 +198,13 @@ SFM_DEV void batcher16(T (&q)[16]) {
 #pragma unroll
         for (int i = 0; i < kk; ++i) {
           const int a = i + j, c = i + j + kk;
-          if (c < 16 && a / (2 * p) == c / (2 * p)) {
-            const T lo = q[a] < q[c] ? q[a] : q[c];
-            const T hi = q[a] < q[c] ? q[c] : q[a];
-            q[a] = lo;
-            q[c] = hi;
-          }
+          if (c < 16 && a / (2 * p) == c / (2 * p)) cas_up(q[a], q[c]);
         }
 }
 
-template <int WS, int ROT>
+// ABL (timing ablations, results invalid): 1 no sort, 2 no prefix chain, 4 no cells, 8 no gradients,
+// 16 no orientation-edge search, 32 no cell-edge keys, 64 no patch loads
+template <int WS, int ROT, int ABL = 0>
 __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl, int H, int W, KpList kp,
                                                    int kcap, const int32_t* __restrict__ lc_all, int level,
                                                    int B, double scale, int32_t* __restrict__ out_xy,
@@ -225,16 +239,16 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
     const int gy = y - h + pr, gx = x - h + pc;
     const bool in = gy >= 0 && gy < H && gx >= 0 && gx < W;
     const int cy = min(max(gy, 0), H - 1), cx = min(max(gx, 0), W - 1);
-    const float v = img[(int64_t)cy * W + cx];
+    const float v = (ABL & 64) ? (float)(cy + cx) : img[(int64_t)cy * W + cx];
     if (e0 < NP) sA[e] = in ? v : 0.0f;
   }
   __syncthreads();
 
   // 2. gradient magnitude / orientation (ScaleRotInvSIFT.py:40-42)
-  uint64_t k[E];
+  double k[E];
   bool tiny = false;
 #pragma unroll
-  for (int r = 0; r < E; ++r) k[r] = ~0ull;
+  for (int r = 0; r < E; ++r) k[r] = __longlong_as_double((long long)kPad);
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
     const int e0 = r * 16 + gl;
@@ -242,13 +256,18 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
     const int e = ok ? e0 : N - 1;
     const int i = e / WS, j = e - i * WS;
     float mag, ori;
-    grad_at(sA + (i + 1) * PW + (j + 1), PW, mag, ori);
+    if constexpr ((ABL & 8) != 0) {
+      mag = sA[(i + 1) * PW + (j + 1)];
+      ori = sA[(i + 1) * PW + j] - 100.0f;
+    } else {
+      grad_at(sA + (i + 1) * PW + (j + 1), PW, mag, ori);
+    }
     if (ok) {
       sM[e] = mag;
       if (!ROT) sK[e] = __float_as_uint(ori);
     }
     if (ROT) {
-      k[r] = ok ? (((uint64_t)fkey(ori) << 32) | (uint32_t)e) : ~0ull;
+      k[r] = ok ? dkey(((uint64_t)fkey(ori) << 9) | (uint32_t)e) : __longlong_as_double((long long)kPad);
       tiny |= ok && ori != 0.0f && fabsf(ori) < 0x1p-25f;
     }
   }
@@ -257,13 +276,16 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
   double dom = 0.0;
   if constexpr (ROT) {
     // 3. dominant orientation (ScaleRotInvSIFT.py:24-31): np.histogram's cumulative path
-    merge_level<E, 2>(k, gl);
+    if constexpr ((ABL & 1) == 0) merge_level<E, 2>(k, gl);
     float w[E];
+    uint32_t ke[E], kf[E];  // pixel and fkey at sorted position gl*E + r
 #pragma unroll
     for (int r = 0; r < E; ++r) {
       const int p = gl * E + r;
-      const uint32_t e = p < N ? (uint32_t)k[r] : 0u;
-      w[r] = p < N ? sM[e] : 0.0f;
+      const uint64_t pl = dpayload(k[r]);
+      ke[r] = p < N ? (uint32_t)(pl & 511u) : 0u;
+      kf[r] = (uint32_t)(pl >> 9);
+      w[r] = p < N ? sM[ke[r]] : 0.0f;
     }
     __syncthreads();  // every gather done before sM is overwritten with sorted weights
     // float32 prefix sum in sorted order: lane s adds its E weights, then hands the
@@ -273,7 +295,11 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
     for (int r = 0; r < E; ++r) cw[r] = 0.0f;
     float carry = 0.0f;
     constexpr int NL = (N + E - 1) / E;
-    for (int s = 0; s < NL; ++s) {
+    if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+      for (int r = 0; r < E; ++r) cw[r] = w[r];
+    }
+    for (int s = 0; s < ((ABL & 2) ? 0 : NL); ++s) {
       if (gl == s) {
         float acc = carry;
 #pragma unroll
@@ -290,12 +316,11 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
       const int p = gl * E + r;
       if (p < N) {
         if constexpr (E >= 4) {
-          *reinterpret_cast<uint4*>(sK + p) = make_uint4((uint32_t)(k[r] >> 32), (uint32_t)(k[r + 1] >> 32),
-                                                         (uint32_t)(k[r + 2] >> 32), (uint32_t)(k[r + 3] >> 32));
+          *reinterpret_cast<uint4*>(sK + p) = make_uint4(kf[r], kf[r + 1], kf[r + 2], kf[r + 3]);
           *reinterpret_cast<float4*>(sM + p) = make_float4(w[r], w[r + 1], w[r + 2], w[r + 3]);
           *reinterpret_cast<float4*>(sA + 4 + p) = make_float4(cw[r], cw[r + 1], cw[r + 2], cw[r + 3]);
         } else {
-          sK[p] = (uint32_t)(k[r] >> 32);
+          sK[p] = kf[r];
           sM[p] = w[r];
           sA[4 + p] = cw[r];
         }
@@ -304,7 +329,7 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
 #pragma unroll
     for (int r = 0; r < E; ++r) {
       const int p = gl * E + r;
-      if (p < N) sR[(uint32_t)k[r]] = (uint16_t)p;
+      if (p < N) sR[ke[r]] = (uint16_t)p;
     }
     if (gl == 0) sA[3] = 0.0f;  // cw[q] lives at sA[3 + q]
     __syncthreads();
@@ -312,7 +337,9 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
 #pragma unroll
     for (int t = 0; t < 3; ++t) {
       const int j = gl + 16 * t;
-      if (j <= 36) {
+      if ((ABL & 16) != 0 && j <= 36) {
+        sI[j] = j * N / 37;
+      } else if (j <= 36) {
         const uint32_t T = edge_key(pi_edge(j, 37), 0.0, j == 36);
         int lo = 0;
         constexpr int S0 = pow2ceil(N + 1) / 2;
@@ -352,8 +379,13 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
   }
 
   // 4. the 4 x 4 cells of 4 x 4 px from the window's top-left (:68-76), 8 bins each
-  if (gl < 9) sT[gl] = edge_key(pi_edge(gl, 9), dom, gl == 8);
+  if (gl < 9) sT[gl] = (ABL & 32) ? 0x80000000u + (uint32_t)(dom * 1e6) * gl : edge_key(pi_edge(gl, 9), dom, gl == 8);
   __syncthreads();  // (also: the rotate prefix sums in sA are no longer read)
+  float hv[8];
+  if constexpr ((ABL & 4) != 0) {
+#pragma unroll
+    for (int bb = 0; bb < 8; ++bb) hv[bb] = sM[gl * 8 + bb] + __uint_as_float(sT[bb & 7]);
+  } else {
   const int r4 = gl >> 2, c4 = gl & 3;
   float wv[16];
   uint32_t hk[16];
@@ -388,7 +420,16 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
       q[t] = ok ? (((uint64_t)key << 32) | (uint32_t)t) : ~0ull;
     }
     if (!ROT) {
-      batcher16(q);
+      double dq16[16];
+#pragma unroll
+      for (int t = 0; t < 16; ++t) dq16[t] = q[t] == ~0ull ? __longlong_as_double((long long)kPad)
+                                                           : dkey(((q[t] >> 32) << 4) | (uint32_t)t);
+      batcher16(dq16);
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const uint64_t pl = dpayload(dq16[t]);
+        q[t] = pl >= (1ull << 36) ? ~0ull : (((pl >> 4) << 32) | (pl & 15u));
+      }
     } else {
       double cv[16];
       int sl[16];
@@ -447,10 +488,10 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
     for (int m = 0; m < 16; ++m) c += hk[m] < T ? 1 : 0;
     bidx[eb] = c;
   }
-  float hv[8];
 #pragma unroll
   for (int bb = 0; bb < 8; ++bb) hv[bb] = cc[bidx[bb + 1]] - cc[bidx[bb]];
 
+  }
   // 5. fixed-order L2 norm: the one-keypoint kernel's tree (lane i holds bins i, i+64,
   //    then halving strides 32..1) — bin 8*cell + t lives in lane `cell`, register t
   float tr[8];
@@ -490,8 +531,7 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
 
 }  // namespace dq
 
-#define SFM_DQ_CASE(WS)                                                                              \
-  case WS:                                                                                           \
+#define SFM_DQ_BODY(WS)                                                                              \
     if (rotate)                                                                                      \
       hipLaunchKernelGGL((dq::k_describe_q<WS, 1>), grid, dim3(64), 0, st, lvl, H, W, kp, kcap, lc,  \
                          level, B, scale, out_xy, out_desc, out_conf, out_cap);                      \
@@ -499,6 +539,9 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
       hipLaunchKernelGGL((dq::k_describe_q<WS, 0>), grid, dim3(64), 0, st, lvl, H, W, kp, kcap, lc,  \
                          level, B, scale, out_xy, out_desc, out_conf, out_cap);                      \
     return true;
+#define SFM_DQ_CASE(WS) \
+  case WS:              \
+    SFM_DQ_BODY(WS)
 
 bool launch_describe_quad(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp, int kcap,
                           const int32_t* lc, int level, double scale, int32_t* out_xy, float* out_desc,
@@ -513,7 +556,33 @@ bool launch_describe_quad(const float* lvl, int B, int H, int W, int fw, int rot
     SFM_DQ_CASE(12)
     SFM_DQ_CASE(14)
     SFM_DQ_CASE(16)
-    SFM_DQ_CASE(18)
+    case 18:
+      if (rotate) {
+        static const int abl = [] {
+          const char* v = getenv("SFMFEAT_DQ_ABL");
+          return v ? atoi(v) : 0;
+        }();
+        switch (abl) {
+#define SFM_DQ_ABL(A)                                                                                     \
+  case A:                                                                                                \
+    hipLaunchKernelGGL((dq::k_describe_q<18, 1, A>), grid, dim3(64), 0, st, lvl, H, W, kp, kcap, lc, level, \
+                       B, scale, out_xy, out_desc, out_conf, out_cap);                                   \
+    return true;
+          SFM_DQ_ABL(1)
+          SFM_DQ_ABL(2)
+          SFM_DQ_ABL(4)
+          SFM_DQ_ABL(8)
+          SFM_DQ_ABL(7)
+          SFM_DQ_ABL(16)
+          SFM_DQ_ABL(32)
+          SFM_DQ_ABL(64)
+          SFM_DQ_ABL(55)
+          SFM_DQ_ABL(127)
+          default:
+            break;
+        }
+      }
+      SFM_DQ_BODY(18)
     SFM_DQ_CASE(20)
     SFM_DQ_CASE(22)
     default:

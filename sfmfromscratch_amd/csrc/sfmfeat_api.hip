@@ -54,10 +54,12 @@ struct sfm_ctx {
   DevBuf m_desc, m_count, m_pairs, m_descT, m_rows, m_matches, m_conf, m_nmatch;
   DevBuf m_hi, m_lo, m_norm2, m_rnorm, m_imgmax;
   bool match_direct = false;  // SFMFEAT_MATCH_DIRECT=1: all-pairs exact VALU kernel (A/B checks)
-  bool exact_select = false;  // SFMFEAT_SELECT=exact: every plane takes the exact-median path
+  bool exact_select = false;
+  bool serial = false;        // SFMFEAT_SERIAL=1: no aux-stream overlap (diagnostic timings)  // SFMFEAT_SELECT=exact: every plane takes the exact-median path
   int last_B = 0;             // planes per level of the last extraction
   // stage profiling (sfm_profile_*): HIP events bracketing each stage's launches
   bool prof = false;
+  uint32_t prof_mask = ~0u;  // stages bracketed while profiling (sfm_profile_stages)
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
   std::vector<hipEvent_t> prof_pool;
   double prof_ms[SFM_PROF_STAGES] = {0};
@@ -84,14 +86,14 @@ struct StageScope {
   hipStream_t st;
   hipEvent_t a = nullptr, b = nullptr;
   StageScope(sfm_ctx* c_, int stage_, hipStream_t st_) : c(c_), stage(stage_), st(st_) {
-    if (c->prof) {
+    if (c->prof && ((c->prof_mask >> stage) & 1u)) {
       a = prof_event(c);
       b = prof_event(c);
       (void)hipEventRecord(a, st);
     }
   }
   ~StageScope() {
-    if (c->prof) {
+    if (a) {
       (void)hipEventRecord(b, st);
       c->prof_pending.push_back({stage, {a, b}});
     }
@@ -252,7 +254,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   // descriptors run on the caller's stream once its Harris work is done.  Descriptors of
   // level l need the keypoint counts of levels < l (slot offsets): ev[L + 2 + l].
   hipStream_t ax = c->aux;
-  const int L_aux = std::min(L, 2);
+  const int L_aux = c->serial ? 0 : std::min(L, 2);  // SFMFEAT_SERIAL=1: one stream (isolated timings)
   HIPCHK(c, hipEventRecord(c->ev[L], st));
   HIPCHK(c, hipStreamWaitEvent(ax, c->ev[L], 0));
   const int rotate = c->p.mode == SFM_MODE_NAIVE ? 0 : 1;
@@ -331,7 +333,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     }
   }
   for (int l = L_aux; l < L; ++l) select_level(l, st);
-  if (L > L_aux) HIPCHK(c, hipStreamWaitEvent(st, c->ev[L + 2], 0));
+  if (L_aux > 0 && L > L_aux) HIPCHK(c, hipStreamWaitEvent(st, c->ev[L + 2], 0));
   for (int l = L_aux; l < L; ++l) describe_level(l, st);
   // join: the caller's stream waits for the aux work
   HIPCHK(c, hipEventRecord(c->ev[L + 1], ax));
@@ -458,6 +460,8 @@ int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out) {
     c->match_direct = e && e[0] == '1';
     const char* se = getenv("SFMFEAT_SELECT");
     c->exact_select = se && strcmp(se, "exact") == 0;
+    const char* sr = getenv("SFMFEAT_SERIAL");
+    c->serial = sr && sr[0] == '1';
   }
   c->cap = (int64_t)c->L * k;
   int gs = p->gaussian_size;
@@ -629,6 +633,14 @@ int32_t sfm_match(sfm_ctx* c, const float* d1, int64_t n1, const float* d2, int6
 int32_t sfm_profile_enable(sfm_ctx* c, int32_t on) {
   if (!c) return SFM_EINVAL;
   c->prof = on != 0;
+  c->prof_mask = ~0u;
+  return SFM_OK;
+}
+
+int32_t sfm_profile_stages(sfm_ctx* c, int32_t mask) {
+  if (!c) return SFM_EINVAL;
+  c->prof = mask != 0;
+  c->prof_mask = (uint32_t)mask;
   return SFM_OK;
 }
 
