@@ -6,6 +6,10 @@ Workload (BASELINE.json configs[1]): per GPU, a batch of 32 synthetic 1080p fram
 "octave" parameters (4 levels x 2, k 2500, ksize 3, 7x7 Gaussian sigma 6, alpha 0.05,
 feature width 18), then NNRatioFeatureMatcher(0.85) over consecutive pairs — the
 reference's schedule (Runner.py:183).  One step = extract the batch + match its pairs.
+Steps go through pipeline.BatchPipeline with --inflight (default 2) batches on the GPU at
+once: each in-flight batch has its own context, stream and slot table, so one batch's
+small pyramid levels, descriptors and matcher overlap the next batch's Harris work.
+Every batch is still fully extracted and matched; --inflight 1 serialises them.
 
 Multi-GPU (weak scaling, one process per GPU, torchrun): rank r owns frames
 [r*B, (r+1)*B) of one global sequence (sfmfromscratch_amd/distributed.py).  The only
@@ -96,6 +100,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=2,
                     help="frames per host thread in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="disable the live per-stage HIP events")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="batches in flight (double-buffered contexts / slot tables, pipeline.BatchPipeline)")
     args = ap.parse_args()
 
     import torch
@@ -111,36 +117,29 @@ def main():
 
     from sfmfromscratch_amd import distributed as D
     from sfmfromscratch_amd import synth
-    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, SlotTable
+    from sfmfromscratch_amd.pipeline import BatchPipeline
 
     B = args.batch
-    ex = BatchExtractor(P_OCT, device=local)
-    cap = ex.cap
-    ex.reserve(B, H, W)
-    matcher = BatchMatcher(RATIO, device=local, ctx=ex.ctx)
-
     # device-resident float32 frames of this rank's shard of the global sequence
     frames_u8 = np.stack([synth.make_frame_u8(H, W, 1234, rank * B + i) for i in range(B)])
     frames = torch.from_numpy(synth.u8_to_gray(frames_u8)).to(dev)
     del frames_u8
-    slots = SlotTable(torch, B + 1, cap, dev)           # slot B = next rank's first frame (halo)
     pairs_np = D.local_consecutive_pairs(B, rank, world)
     pairs = torch.from_numpy(pairs_np).to(dev)
     P = pairs.shape[0]
-    mout = (torch.zeros((P, cap, 2), dtype=torch.int32, device=dev),
-            torch.zeros((P, cap), dtype=torch.float32, device=dev),
-            torch.zeros((P,), dtype=torch.int32, device=dev))
+    # slot B of each lane's table = the next rank's first frame (halo)
+    pipe = BatchPipeline(P_OCT, RATIO, B, H, W, pairs, inflight=args.inflight, device=local, extra_slots=1)
+    ctxs = pipe.contexts
 
-    class View:  # the first B rows of the slot table, as the extractor's output
-        xy, desc, count = slots.xy[:B], slots.desc[:B], slots.count[:B]
+    def halo(slots, n):
+        D.halo_exchange(dist, slots, n, rank, world)
 
     def step():
-        ex.extract(frames, out=View)
-        D.halo_exchange(dist, slots, B, rank, world)
-        matcher.match(slots, pairs, out=mout)
+        pipe.submit(frames, hook=halo)
 
     for _ in range(args.warmup):
         step()
+    pipe.join()
     torch.cuda.synchronize()
 
     def stage_work(counts, nsteps):
@@ -158,17 +157,35 @@ def main():
             "describe": ("hbm", DESC_BYTES_PER_KP * kps / 1e9, "GB/s", PEAK_HBM_GBS),
         }
 
-    # Per-stage device times (every stage bracketed by HIP events) in an untimed pass; it
-    # names the dominant stage, whose events alone stay on during the timed run.
+    def prof_enable(on):
+        for c in ctxs:
+            c.profile_enable(on)
+
+    def prof_read():
+        tot = {}
+        for c in ctxs:
+            for k, (ms, n) in c.profile_read(reset=True).items():
+                a = tot.get(k, (0.0, 0))
+                tot[k] = (a[0] + ms, a[1] + n)
+        return tot
+
+    def lane_counts():
+        return pipe.lanes[0]["slots"].count.cpu().numpy()
+
+    # Per-stage device times (every stage bracketed by HIP events) in an untimed pass with
+    # one batch on the GPU at a time; it names the dominant stage, whose events alone
+    # stay on during the timed run.
     stages, dom = {}, None
     if not args.no_profile:
         nprof = max(2, args.steps // 2)
-        ex.ctx.profile_enable(True)
-        ex.ctx.profile_read(reset=True)
+        prof_enable(True)
+        prof_read()
         for _ in range(nprof):
             step()
-        prof_all = ex.ctx.profile_read(reset=True)
-        work = stage_work(slots.count.cpu().numpy(), nprof)
+            pipe.join()
+            torch.cuda.synchronize()
+        prof_all = prof_read()
+        work = stage_work(lane_counts(), nprof)
         for k, (ms, n) in prof_all.items():
             if not n:
                 continue
@@ -179,8 +196,9 @@ def main():
                 st.update({"bound": bound, "achieved": round(ach, 3), "unit": unit, "frac": round(ach / peak, 4)})
             stages[k] = st
         dom = max((k for k in prof_all if k in work and prof_all[k][1]), key=lambda k: prof_all[k][0])
-        ex.ctx.profile_stages([dom])
-        ex.ctx.profile_read(reset=True)
+        for c in ctxs:
+            c.profile_stages([dom])
+        prof_read()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -188,8 +206,10 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record()
+    pipe.start()
     for _ in range(args.steps):
         step()
+    pipe.join()
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -202,10 +222,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
-    prof = ex.ctx.profile_read(reset=True) if dom else {}
-    ex.ctx.profile_enable(False)
-    counts = slots.count.cpu().numpy()
-    nmatch = mout[2].cpu().numpy()
+    prof = prof_read() if dom else {}
+    prof_enable(False)
+    counts = lane_counts()
+    nmatch = pipe.lanes[0]["mout"][2].cpu().numpy()
 
     images = world * B * args.steps
     value = images / elapsed
@@ -224,7 +244,8 @@ def main():
         roof = {"kernel": kname, "stage": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak,
                 "unit": unit, "frac": round(achieved / peak, 4), "traffic": tr,
                 "avg_launch_ms": round(ms / max(n, 1), 4), "launches": n,
-                "timing": "HIP events around each launch of the stage inside the timed region"}
+                "timing": "HIP events around each launch of the stage inside the timed region "
+                          f"({args.inflight} batches in flight)"}
         if tr is not None:
             roof["traffic_note"] = "HBM bytes per launch, rocprofv3 PMC (profiles/pmc_traffic.json)"
 
@@ -255,7 +276,7 @@ def main():
                        "frames_per_gpu": B, "image": [H, W], "pairs_per_gpu": int(P),
                        "keypoints_mean": float(np.mean(counts[:B])),
                        "matches_mean": float(np.mean(nmatch[nmatch >= 0])) if (nmatch >= 0).any() else 0.0,
-                       "parallelism": f"image-shard x{world}"},
+                       "parallelism": f"image-shard x{world}", "batches_in_flight": args.inflight},
             "roofline": roof,
             "cpu_baseline": cpu,
             "stages_ms": stages,

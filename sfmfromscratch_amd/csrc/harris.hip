@@ -3,270 +3,346 @@
 // window sums -> R = det - alpha * trace^2, plus the first radix digit histogram of R
 // for the exact median (NaiveSIFT.py:91).
 //
-// One workgroup (256 threads, 4 waves) walks 64 x 32 output tiles of one plane.  The three
-// product planes of a tile (+ window halo) live in LDS; each thread accumulates 4 pixels x
-// 2 rows with packed fp32 fmas (v_pk_fma_f32: the two rows' taps as one SGPR pair, the LDS
-// value broadcast).  The 2-D window is the
-// reference's full KS x KS correlation (not separable: a separable sum would round
-// differently and move keypoints), accumulated per pixel as an fma chain
-// in row-major tap order (OpenCV FilterVec_32f's v_muladd chain).
+// One workgroup (256 threads) walks 64 x 64 output tiles of one plane (see k_harris).  The
+// 2-D window is the reference's full KS x KS correlation (not separable: a separable sum
+// would round differently and move keypoints), accumulated per pixel as an
+// fma chain in row-major tap order (OpenCV FilterVec_32f's v_muladd chain; DESIGN.md
+// §Numerics).
 // VALU-bound by design.
 #include <algorithm>
+#include <utility>
 
 #include "kernels.h"
 
 namespace sfm {
 
-constexpr int kHT_W = 64;   // output tile width  (16 thread columns x 4 pixels)
-constexpr int kHT_H = 32;   // output tile height (16 thread row pairs x 2 rows)
+// static_for<N>(f): f(std::integral_constant<int, 0>{}) ... f(<N-1>{}), fully expanded
+// (the window loop body is too large for the unroll pragma, and its taps must be
+// compile-time indices to stay in SGPRs)
+template <int... I, class F>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+constexpr int kHT = 64;   // output tile: 64 x 64 pixels (16 column groups x 16 row quads)
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // acc = (k.x, k.y) * (v[H], v[H]) + acc : one v_pk_fma_f32 (two IEEE fmas, each bitwise
-// fmaf) with the LDS value broadcast to both halves by op_sel — no register shuffles.
+// fmaf) with the product value broadcast to both halves by op_sel — no register shuffles.
 template <int H>
 __device__ __forceinline__ void pk_fma_bcast(f32x2& acc, f32x2 k, f32x2 v) {
   if constexpr (H == 0)
-    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "s"(k), "v"(v));
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "v"(k), "v"(v));
   else
-    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "s"(k), "v"(v));
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(k), "v"(v));
 }
 
-// ABL (ablation, timing builds only): 0 = full kernel, 1 = no digit histogram,
-// 2 = no window sums, 3 = no Sobel/products (image copied into the product planes),
-// 4 = image load + R store only, 5 = R store only
-template <int KS, int ABL = 0>
-__global__ void __launch_bounds__(256) k_harris(const float* __restrict__ lvl, float* __restrict__ Rout,
-                                                uint32_t* __restrict__ hist_g, int H, int W,
-                                                int tiles_x, int ntiles,
-                                                const float* __restrict__ gk, float alpha,
-                                                SelectScan scan) {
+// One workgroup (256 threads, 4 waves, 2 per CU) walks 64 x 64 output tiles of one plane.
+// LDS holds the image tile (+ Sobel and window halo) and the two gradient planes Ix, Iy of
+// the tile + window halo.  Each thread owns 4 columns x 4 rows: for every LDS gradient row
+// it forms the three products Ix^2, Iy^2, IxIy in registers (v_pk_mul_f32; the same IEEE
+// products the reference's elementwise multiplies give) and feeds them to all 4 output
+// rows' window sums, as two row pairs of packed fmas.  LDS traffic per window fma is ~5x
+// below a one-plane-per-product, 2-row layout, which left the kernel LDS-bound.
+//
+// VEC (W % 4 == 0): the image tile is fetched as 16-B loads (its left edge sits XA columns
+// left of the tile, XA = round_up(GA + 1, 4), so every float4 is either wholly inside the
+// image or wholly outside); otherwise scalar loads.  Both variants are prefetched into
+// registers one tile ahead.
+//
+// ABL (timing builds only): 0 = full kernel, 1 = no digit histogram, 2 = window sums over
+// the first tap row only.
+template <int KS, bool VEC, int ABL = 0>
+__global__ void __launch_bounds__(256, 2) k_harris(const float* __restrict__ lvl, float* __restrict__ Rout,
+                                                   uint32_t* __restrict__ hist_g, int H, int W,
+                                                   int tiles_x, int ntiles,
+                                                   const float* __restrict__ gk, float alpha,
+                                                   SelectScan scan) {
   constexpr int GA = KS / 2;
-  constexpr int PW = kHT_W + KS - 1;        // product tile width
-  constexpr int PH = kHT_H + KS - 1;        // product tile height
-  // product row stride S == 8 (mod 32) floats: with lane = 4*rp + (tq & 3) every 16-lane
-  // group of a ds_read_b128 ({0-3,12-15,20-27}, ...) covers 4 row pairs x 4 column
-  // groups, whose 16-B chunks 4*rp + tq (mod 16) are all distinct -> conflict-free
-  constexpr int PWP = (PW <= 72) ? 72 : (PW <= 104 ? 104 : 136);
-  constexpr int NV = 4 + KS - 1;            // window values per row per plane
-  constexpr int NV4 = (NV + 3) / 4;         // b128 loads per row per plane
+  constexpr int PH = kHT + KS - 1;          // gradient rows of a tile (window halo)
+  constexpr int NV = 4 + KS - 1;            // gradient values per row per thread
+  constexpr int NV4 = (NV + 3) / 4;         // b128 LDS loads per row per plane
   constexpr int NVP = 4 * NV4;
-  static_assert(PWP >= PW && 60 + NVP <= PWP, "harris LDS row stride");
-  constexpr int NS = PWP / 4;               // 4-wide product strips per product row
-  constexpr int IH = PH + 2;                // image tile (Sobel halo)
-  constexpr int IWP = PWP + 4;              // covers every strip's 8-float read
-  constexpr int NIMG = (IH * IWP + 255) / 256;
-  constexpr int SRW = kHT_W + 4;            // R staging row stride (in the image tile)
-  static_assert(IH * IWP >= kHT_H * SRW, "R staging fits in the image tile");
-  static_assert(NIMG <= 32, "prefetch mask");
-  __shared__ __attribute__((aligned(16))) float s_prod[3][PH][PWP];
+  constexpr int NP2 = (NV + 1) / 2;         // product pairs per row
+  // gradient row stride == 8 (mod 32) floats: a 16-lane group of a ds_read_b128 holds
+  // 8 column groups x 2 row quads, whose 16-B chunks 8*rq + tq (mod 16) are distinct
+  constexpr int PWP = (kHT + KS - 1 <= 72 && 60 + NVP <= 72) ? 72 : ((60 + NVP <= 104) ? 104 : 136);
+  static_assert(PWP >= kHT + KS - 1 && 60 + NVP <= PWP, "harris LDS row stride");
+  constexpr int NS = PWP / 4;               // 4-wide gradient strips per row
+  constexpr int XA = (GA + 1 + 3) / 4 * 4;  // image tile margin left of the output tile
+  constexpr int SH = XA - GA - 1;           // image column of gradient column 0, minus 1
+  constexpr int NR4 = (SH + 6 + 3) / 4;     // float4 reads per Sobel strip row
+  constexpr int IH = PH + 2;                // image tile rows (Sobel halo)
+  constexpr int IWP = PWP + 4 * (NR4 - 1);  // covers every strip's reads
+  constexpr int IW4 = IWP / 4;
+  constexpr int NIMG = VEC ? (IH * IW4 + 255) / 256 : (IH * IWP + 255) / 256;
+  static_assert(NIMG <= 64, "prefetch mask");
+  __shared__ __attribute__((aligned(16))) float s_g[2][PH][PWP];
   __shared__ __attribute__((aligned(16))) float s_img[IH][IWP];
   __shared__ uint32_t s_hist[kMedBins1];  // digit-1 histogram, flushed once per workgroup
+  // tap pairs per gradient row r and row pair p: (g[r-2p][j], g[r-2p-1][j]), 0 where the
+  // tap row does not exist; read as uniform LDS broadcasts (49 taps in SGPRs spill)
+  __shared__ __attribute__((aligned(16))) f32x2 s_tp[KS + 3][2][KS + (KS & 1)];
   __shared__ uint32_t s_last, s_red[8];
 
   const int tid = threadIdx.x;
   const int b = blockIdx.y;
   const float* img = lvl + (int64_t)b * H * W;
+  float* Rp = Rout + (int64_t)b * H * W;
   for (int i = tid; i < kMedBins1; i += 256) s_hist[i] = 0u;
-  const int lane = tid & 63;
-  const int rp = lane >> 2;                      // row pair: output rows 2rp, 2rp+1
-  const int tq = ((tid >> 6) << 2) | (lane & 3); // pixel columns 4tq .. 4tq+3
-  // image tile loads for `tile` into registers (clamped, always-valid addresses; zero
-  // outside the image = BORDER_CONSTANT).  Issued one tile ahead so their latency hides
-  // under the previous tile's window sums.
-  float t[NIMG];
-  uint32_t okmask = 0;
+  for (int i = tid; i < (KS + 3) * 2 * KS; i += 256) {
+    const int r = i / (2 * KS), p = (i / KS) & 1, j = i % KS;
+    const int i0 = r - 2 * p, i1 = i0 - 1;
+    s_tp[r][p][j] = f32x2{(i0 >= 0 && i0 < KS) ? gk[i0 * KS + j] : 0.0f, (i1 >= 0 && i1 < KS) ? gk[i1 * KS + j] : 0.0f};
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+  const int tq = (lane & 7) | ((wv & 1) << 3);          // columns 4tq .. 4tq+3
+  const int rq = ((lane >> 3) & 7) | ((wv >> 1) << 3);  // rows 4rq .. 4rq+3
+
+  // image tile of `tile` -> registers (zero outside the image = BORDER_CONSTANT)
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  f32x4 t4[VEC ? NIMG : 1];
+  float t1[VEC ? 1 : NIMG];
+  uint64_t okmask = 0;
   auto prefetch = [&](int tile) {
-    const int px0 = (tile % tiles_x) * kHT_W - GA - 1;
-    const int py0 = (tile / tiles_x) * kHT_H - GA - 1;
+    const int gx0 = (tile % tiles_x) * kHT - XA;
+    const int gy0 = (tile / tiles_x) * kHT - GA - 1;
     okmask = 0;
+    if constexpr (VEC) {
 #pragma unroll
-    for (int k = 0; k < NIMG; ++k) {
-      const int idx = tid + 256 * k;
-      const int iy = idx / IWP, ix = idx - iy * IWP;
-      const int gy = py0 + iy, gx = px0 + ix;
-      const int yc = min(max(gy, 0), H - 1), xc = min(max(gx, 0), W - 1);
-      t[k] = img[(int64_t)yc * W + xc];
-      okmask |= (idx < IH * IWP && gy >= 0 && gy < H && gx >= 0 && gx < W) ? (1u << k) : 0u;
+      for (int k = 0; k < NIMG; ++k) {
+        const int e = tid + 256 * k;
+        const int iy = e / IW4, gx = gx0 + 4 * (e - iy * IW4), gy = gy0 + iy;
+        const bool ok = e < IH * IW4 && gy >= 0 && gy < H && gx >= 0 && gx < W;
+        const int64_t off = ok ? (int64_t)gy * W + gx : 0;
+        t4[k] = *reinterpret_cast<const f32x4*>(img + off);
+        okmask |= ok ? (1ull << k) : 0ull;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NIMG; ++k) {
+        const int e = tid + 256 * k;
+        const int iy = e / IWP, gx = gx0 + (e - iy * IWP), gy = gy0 + iy;
+        const bool ok = e < IH * IWP && gy >= 0 && gy < H && gx >= 0 && gx < W;
+        t1[k] = img[ok ? (int64_t)gy * W + gx : 0];
+        okmask |= ok ? (1ull << k) : 0ull;
+      }
     }
   };
-  if (ABL != 5 && blockIdx.x < ntiles) prefetch(blockIdx.x);
+  if (blockIdx.x < ntiles) prefetch(blockIdx.x);
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int tx0 = (tile % tiles_x) * kHT_W;
-    const int ty0 = (tile / tiles_x) * kHT_H;
-    __syncthreads();  // previous tile's LDS reads are done
-    // 0. the prefetched image tile -> LDS
+    const int tx0 = (tile % tiles_x) * kHT;
+    const int ty0 = (tile / tiles_x) * kHT;
+    __syncthreads();  // the previous tile's LDS reads are done
+    // 0. the prefetched image tile -> LDS, then start fetching the next tile
 #pragma unroll
     for (int k = 0; k < NIMG; ++k) {
-      const int idx = tid + 256 * k;
-      if (idx < IH * IWP) (&s_img[0][0])[idx] = (okmask >> k) & 1u ? t[k] : 0.0f;
+      const bool ok = (okmask >> k) & 1ull;
+      if constexpr (VEC) {
+        const int e = tid + 256 * k;
+        if (e < IH * IW4)
+          reinterpret_cast<f32x4*>(&s_img[0][0])[e] = ok ? t4[k] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      } else {
+        const int e = tid + 256 * k;
+        if (e < IH * IWP) (&s_img[0][0])[e] = ok ? t1[k] : 0.0f;
+      }
     }
     __syncthreads();
+    if (tile + (int)gridDim.x < ntiles) prefetch(tile + gridDim.x);
     // 1. gradients (NaiveSIFT.py:201-213: fma chain over the non-zero Sobel taps in
-    //    row-major order from +0; k*p is exact for these taps) and products Ix^2, Iy^2,
-    //    IxIy (:61-63) for 4-wide strips; consecutive lanes fill consecutive 16-B chunks
-    //    (row stride == strip count * 4), outside the image -> 0
-    for (int sidx = tid; sidx < PH * NS; sidx += 256) {
-      if (ABL >= 4) break;
-      const int py = sidx / NS, px0 = (sidx - py * NS) * 4;
-      if (ABL == 3) {
+    //    row-major order from +0; k*p is exact for these taps) for 4-wide strips; outside
+    //    the image the gradients are 0, so their products (:61-63) are the zero border of
+    //    the window sums (:67-69)
+    //    Packed over column pairs (q, q+1) when the strip's image reads are pair-aligned
+    //    (each half an IEEE fma, as the scalar chain); interior tiles skip the masking.
+    auto sobel = [&](auto maskedc) {
+      constexpr bool MASKED = decltype(maskedc)::value;
+      for (int sidx = tid; sidx < PH * NS; sidx += 256) {
+        const int py = sidx / NS, px0 = (sidx - py * NS) * 4;
+        f32x2 w[3][2 * NR4];
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-          *reinterpret_cast<float4*>(&s_prod[pl][py][px0]) =
-              *reinterpret_cast<const float4*>(&s_img[py + 1][px0]);
-        continue;
-      }
-      float w[3][8];
+        for (int dy = 0; dy < 3; ++dy) {
+          const float4* row = reinterpret_cast<const float4*>(&s_img[py + dy][px0]);
 #pragma unroll
-      for (int dy = 0; dy < 3; ++dy) {
-        const float4* row = reinterpret_cast<const float4*>(&s_img[py + dy][px0]);
-#pragma unroll
-        for (int c4 = 0; c4 < 2; ++c4) {
-          const float4 v = row[c4];
-          w[dy][4 * c4 + 0] = v.x;
-          w[dy][4 * c4 + 1] = v.y;
-          w[dy][4 * c4 + 2] = v.z;
-          w[dy][4 * c4 + 3] = v.w;
-        }
-      }
-      const int gy = ty0 - GA + py;
-      const bool rowin = gy >= 0 && gy < H;
-      float pxx[4], pyy[4], pxy[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int gx = tx0 - GA + px0 + q;
-        float ix = 0.0f;
-        ix = __builtin_fmaf(-1.0f, w[0][q], ix);
-        ix = __builtin_fmaf(1.0f, w[0][q + 2], ix);
-        ix = __builtin_fmaf(-2.0f, w[1][q], ix);
-        ix = __builtin_fmaf(2.0f, w[1][q + 2], ix);
-        ix = __builtin_fmaf(-1.0f, w[2][q], ix);
-        ix = __builtin_fmaf(1.0f, w[2][q + 2], ix);
-        float iy = 0.0f;
-        iy = __builtin_fmaf(-1.0f, w[0][q], iy);
-        iy = __builtin_fmaf(-2.0f, w[0][q + 1], iy);
-        iy = __builtin_fmaf(-1.0f, w[0][q + 2], iy);
-        iy = __builtin_fmaf(1.0f, w[2][q], iy);
-        iy = __builtin_fmaf(2.0f, w[2][q + 1], iy);
-        iy = __builtin_fmaf(1.0f, w[2][q + 2], iy);
-        const bool inside = rowin && gx >= 0 && gx < W;
-        pxx[q] = inside ? ix * ix : 0.0f;
-        pyy[q] = inside ? iy * iy : 0.0f;
-        pxy[q] = inside ? ix * iy : 0.0f;
-      }
-      *reinterpret_cast<float4*>(&s_prod[0][py][px0]) = make_float4(pxx[0], pxx[1], pxx[2], pxx[3]);
-      *reinterpret_cast<float4*>(&s_prod[1][py][px0]) = make_float4(pyy[0], pyy[1], pyy[2], pyy[3]);
-      *reinterpret_cast<float4*>(&s_prod[2][py][px0]) = make_float4(pxy[0], pxy[1], pxy[2], pxy[3]);
-    }
-    __syncthreads();
-
-    if (ABL != 5 && tile + (int)gridDim.x < ntiles) prefetch(tile + gridDim.x);
-    // 2. window sums (:67-69): per pixel an fma chain over the KS x KS taps in row-major
-    //    order.  acc[pl][q] = (row 2rp, row 2rp+1) at column 4tq+q; LDS row 2rp+i feeds
-    //    tap row i of the first and tap row i-1 of the second, so rows 1..KS-1 are packed
-    //    fmas and the first / last rows are scalar fmas on one half.
-    f32x2 acc[3][4];
-#pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc[pl][q] = f32x2{0.0f, 0.0f};
-    auto load_row = [&](int pl, int i, f32x2 (&v)[NVP / 2]) {
-      const float4* row = reinterpret_cast<const float4*>(&s_prod[pl][2 * rp + i][4 * tq]);
-#pragma unroll
-      for (int c4 = 0; c4 < NV4; ++c4) {
-        const float4 t4 = row[c4];
-        v[2 * c4] = f32x2{t4.x, t4.y};
-        v[2 * c4 + 1] = f32x2{t4.z, t4.w};
-      }
-    };
-    constexpr int NWR = (ABL == 2) ? 1 : (ABL >= 4 ? 0 : KS);  // tap rows
-    constexpr int NWC = (ABL == 2) ? 1 : KS;                    // taps per row
-    if constexpr (NWR > 0) {
-      // LDS row 0: tap row 0 of the first row only
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
-        f32x2 v[NVP / 2];
-        load_row(pl, 0, v);
-#pragma unroll
-        for (int j = 0; j < NWC; ++j) {
-          const float kk = gk[j];
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            acc[pl][q].x = __builtin_fmaf(kk, v[(q + j) >> 1][(q + j) & 1], acc[pl][q].x);
-        }
-      }
-#pragma unroll 1
-      for (int i = 1; i < NWR; ++i) {
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          f32x2 v[NVP / 2];
-          load_row(pl, i, v);
-#pragma unroll
-          for (int j = 0; j < NWC; ++j) {
-            const f32x2 k2 = f32x2{gk[i * KS + j], gk[(i - 1) * KS + j]};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              if (((q + j) & 1) == 0)
-                pk_fma_bcast<0>(acc[pl][q], k2, v[(q + j) >> 1]);
-              else
-                pk_fma_bcast<1>(acc[pl][q], k2, v[(q + j) >> 1]);
-            }
+          for (int c4 = 0; c4 < NR4; ++c4) {
+            const float4 v = row[c4];
+            w[dy][2 * c4] = f32x2{v.x, v.y};
+            w[dy][2 * c4 + 1] = f32x2{v.z, v.w};
           }
         }
+        auto val = [&](int dy, int c) { return w[dy][c >> 1][c & 1]; };
+        float gxq[4], gyq[4];
+        if constexpr ((SH & 1) == 0) {
+          const f32x2 m1 = {-1.0f, -1.0f}, p1 = {1.0f, 1.0f}, m2 = {-2.0f, -2.0f}, p2 = {2.0f, 2.0f};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {  // columns (2h, 2h+1)
+            const int c = (2 * h + SH) >> 1;  // pair index of column 2h + SH
+            f32x2 ix = {0.0f, 0.0f}, iy = {0.0f, 0.0f};
+            // the (c+1) pair straddles pairs: (w[c].y, w[c+1].x) is read as columns
+            // q+1; build it only for iy's centre taps
+            const f32x2 mid0 = f32x2{w[0][c].y, w[0][c + 1].x};
+            const f32x2 mid2 = f32x2{w[2][c].y, w[2][c + 1].x};
+            ix = __builtin_elementwise_fma(m1, w[0][c], ix);
+            ix = __builtin_elementwise_fma(p1, w[0][c + 1], ix);
+            ix = __builtin_elementwise_fma(m2, w[1][c], ix);
+            ix = __builtin_elementwise_fma(p2, w[1][c + 1], ix);
+            ix = __builtin_elementwise_fma(m1, w[2][c], ix);
+            ix = __builtin_elementwise_fma(p1, w[2][c + 1], ix);
+            iy = __builtin_elementwise_fma(m1, w[0][c], iy);
+            iy = __builtin_elementwise_fma(m2, mid0, iy);
+            iy = __builtin_elementwise_fma(m1, w[0][c + 1], iy);
+            iy = __builtin_elementwise_fma(p1, w[2][c], iy);
+            iy = __builtin_elementwise_fma(p2, mid2, iy);
+            iy = __builtin_elementwise_fma(p1, w[2][c + 1], iy);
+            gxq[2 * h] = ix.x;
+            gxq[2 * h + 1] = ix.y;
+            gyq[2 * h] = iy.x;
+            gyq[2 * h + 1] = iy.y;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int c = q + SH;
+            float ix = 0.0f;
+            ix = __builtin_fmaf(-1.0f, val(0, c), ix);
+            ix = __builtin_fmaf(1.0f, val(0, c + 2), ix);
+            ix = __builtin_fmaf(-2.0f, val(1, c), ix);
+            ix = __builtin_fmaf(2.0f, val(1, c + 2), ix);
+            ix = __builtin_fmaf(-1.0f, val(2, c), ix);
+            ix = __builtin_fmaf(1.0f, val(2, c + 2), ix);
+            float iy = 0.0f;
+            iy = __builtin_fmaf(-1.0f, val(0, c), iy);
+            iy = __builtin_fmaf(-2.0f, val(0, c + 1), iy);
+            iy = __builtin_fmaf(-1.0f, val(0, c + 2), iy);
+            iy = __builtin_fmaf(1.0f, val(2, c), iy);
+            iy = __builtin_fmaf(2.0f, val(2, c + 1), iy);
+            iy = __builtin_fmaf(1.0f, val(2, c + 2), iy);
+            gxq[q] = ix;
+            gyq[q] = iy;
+          }
+        }
+        if constexpr (MASKED) {
+          const int gy = ty0 - GA + py;
+          const bool rowin = gy >= 0 && gy < H;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int gx = tx0 - GA + px0 + q;
+            const bool inside = rowin && gx >= 0 && gx < W;
+            gxq[q] = inside ? gxq[q] : 0.0f;
+            gyq[q] = inside ? gyq[q] : 0.0f;
+          }
+        }
+        *reinterpret_cast<float4*>(&s_g[0][py][px0]) = make_float4(gxq[0], gxq[1], gxq[2], gxq[3]);
+        *reinterpret_cast<float4*>(&s_g[1][py][px0]) = make_float4(gyq[0], gyq[1], gyq[2], gyq[3]);
       }
-      // LDS row NWR: tap row NWR-1 of the second row only
+    };
+    // every gradient position of the tile (incl. the unused stride padding) in the image
+    const bool grad_in = tx0 - GA >= 0 && tx0 - GA + PWP <= W && ty0 - GA >= 0 && ty0 - GA + PH <= H;
+    if (grad_in) sobel(std::false_type{});
+    else sobel(std::true_type{});
+    __syncthreads();
+
+    // 2. window sums (:67-69): per pixel an fma chain over the KS x KS taps in row-major
+    //    order.  acc[p][pl][q] = (row 4rq+2p, row 4rq+2p+1) at column 4tq+q; gradient row
+    //    4rq+r feeds tap row r-2p of the pair's first row and r-2p-1 of its second: packed
+    //    fmas where both are taps, a scalar fma on one half at the pair's first/last row.
+    f32x2 acc[2][3][4];
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
-        f32x2 v[NVP / 2];
-        load_row(pl, NWR, v);
+    for (int p = 0; p < 2; ++p)
 #pragma unroll
-        for (int j = 0; j < NWC; ++j) {
-          const float kk = gk[(NWR - 1) * KS + j];
+      for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            acc[pl][q].y = __builtin_fmaf(kk, v[(q + j) >> 1][(q + j) & 1], acc[pl][q].y);
+        for (int q = 0; q < 4; ++q) acc[p][pl][q] = f32x2{0.0f, 0.0f};
+    constexpr int NR = (ABL == 2) ? 1 : KS + 3;  // gradient rows feeding this thread
+    static_for<NR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      f32x2 P[3][NP2];
+      {
+        const float4* rx = reinterpret_cast<const float4*>(&s_g[0][4 * rq + r][4 * tq]);
+        const float4* ry = reinterpret_cast<const float4*>(&s_g[1][4 * rq + r][4 * tq]);
+        f32x2 X[NVP / 2], Y[NVP / 2];
+#pragma unroll
+        for (int c4 = 0; c4 < NV4; ++c4) {
+          const float4 a = rx[c4], c = ry[c4];
+          X[2 * c4] = f32x2{a.x, a.y};
+          X[2 * c4 + 1] = f32x2{a.z, a.w};
+          Y[2 * c4] = f32x2{c.x, c.y};
+          Y[2 * c4 + 1] = f32x2{c.z, c.w};
+        }
+#pragma unroll
+        for (int m = 0; m < NP2; ++m) {
+          P[0][m] = X[m] * X[m];
+          P[1][m] = Y[m] * Y[m];
+          P[2][m] = X[m] * Y[m];
         }
       }
-    }
-    // 3. R = det - alpha * trace^2 (:71-74), digit-1 histogram of R; R goes through LDS
-    //    (the image tile's space, dead after step 1) so the global store is coalesced rows
-    float* sR = &s_img[0][0];  // [kHT_H][SRW]
+      f32x2 T[2][KS + (KS & 1)];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int rr = 2 * rp + h;
-      const int gy = ty0 + rr;
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int j2 = 0; j2 < (KS + 1) / 2; ++j2) {
+          const float4 t = *reinterpret_cast<const float4*>(&s_tp[r][p][2 * j2]);
+          T[p][2 * j2] = f32x2{t.x, t.y};
+          T[p][2 * j2 + 1] = f32x2{t.z, t.w};
+        }
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int i0 = r - 2 * p, i1 = r - 2 * p - 1;  // tap rows of the pair's two rows
+        const bool v0 = i0 >= 0 && i0 < KS && (ABL != 2 || i0 == 0);
+        const bool v1 = i1 >= 0 && i1 < KS && ABL != 2;
+        if (!v0 && !v1) continue;  // (a compile-time condition)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+          for (int j = 0; j < KS; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int m = q + j;
+              if (v0 && v1) {
+                if (m & 1) pk_fma_bcast<1>(acc[p][pl][q], T[p][j], P[pl][m >> 1]);
+                else pk_fma_bcast<0>(acc[p][pl][q], T[p][j], P[pl][m >> 1]);
+              } else if (v0) {
+                acc[p][pl][q].x = __builtin_fmaf(T[p][j].x, P[pl][m >> 1][m & 1], acc[p][pl][q].x);
+              } else {
+                acc[p][pl][q].y = __builtin_fmaf(T[p][j].y, P[pl][m >> 1][m & 1], acc[p][pl][q].y);
+              }
+            }
+      }
+    });
+    // 3. R = det - alpha * trace^2 (:71-74), digit-1 histogram of R, R stored as 16-B
+    //    row segments (a wave writes 8 rows x 128 contiguous bytes per store)
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const int gy = ty0 + 4 * rq + o;
+      const int gx0 = tx0 + 4 * tq;
       float Rq[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int gx = tx0 + 4 * tq + q;
-        const float sxx = acc[0][q][h], syy = acc[1][q][h], sxy = acc[2][q][h];
-        const float t1 = sxx * syy;
-        const float t2 = sxy * sxy;
-        const float det = t1 - t2;
+        const float sxx = acc[o >> 1][0][q][o & 1], syy = acc[o >> 1][1][q][o & 1],
+                    sxy = acc[o >> 1][2][q][o & 1];
+        const float t1v = sxx * syy;
+        const float t2v = sxy * sxy;
+        const float det = t1v - t2v;
         const float tr = sxx + syy;
         const float tr2 = tr * tr;
         const float at = alpha * tr2;
-        const float Rv = det - at;
-        Rq[q] = Rv;
-        if (ABL != 1 && gy < H && gx < W) atomicAdd(&s_hist[fkey(Rv) >> (32 - kMedBits1)], 1u);
+        Rq[q] = det - at;
+        if (ABL != 1) atomicAdd(&s_hist[fkey(Rq[q]) >> (32 - kMedBits1)], (gy < H && gx0 + q < W) ? 1u : 0u);
       }
-      *reinterpret_cast<float4*>(&sR[rr * SRW + 4 * tq]) = make_float4(Rq[0], Rq[1], Rq[2], Rq[3]);
-    }
-    __syncthreads();
-    float* Rp = Rout + (int64_t)b * H * W;
-    if ((W & 3) == 0 && tx0 + kHT_W <= W) {
+      if (gy < H) {
+        float* dst = Rp + (int64_t)gy * W + gx0;
+        if (VEC) {
+          if (gx0 < W) *reinterpret_cast<float4*>(dst) = make_float4(Rq[0], Rq[1], Rq[2], Rq[3]);
+        } else {
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int e = tid + 256 * k;            // 512 float4 = 32 rows x 16
-        const int rr = e >> 4, c4 = (e & 15) * 4;
-        if (ty0 + rr < H)
-          *reinterpret_cast<float4*>(Rp + (int64_t)(ty0 + rr) * W + tx0 + c4) =
-              *reinterpret_cast<const float4*>(&sR[rr * SRW + c4]);
-      }
-    } else {
-      for (int e = tid; e < kHT_H * kHT_W; e += 256) {
-        const int rr = e / kHT_W, cc = e - rr * kHT_W;
-        if (ty0 + rr < H && tx0 + cc < W) Rp[(int64_t)(ty0 + rr) * W + tx0 + cc] = sR[rr * SRW + cc];
+          for (int q = 0; q < 4; ++q)
+            if (gx0 + q < W) dst[q] = Rq[q];
+        }
       }
     }
   }  // tile loop
@@ -294,14 +370,18 @@ __global__ void __launch_bounds__(256) k_harris(const float* __restrict__ lvl, f
 template <int KS, int ABL = 0>
 static void launch_ks(const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
                       const float* gk, float alpha, SelectScan scan, hipStream_t st) {
-  int tiles_x = (W + kHT_W - 1) / kHT_W;
-  int tiles_y = (H + kHT_H - 1) / kHT_H;
+  int tiles_x = (W + kHT - 1) / kHT;
+  int tiles_y = (H + kHT - 1) / kHT;
   int ntiles = tiles_x * tiles_y;
-  // ~4 resident workgroups per CU over the whole batch; each loops over tiles so the
+  // 2 resident workgroups per CU over the whole batch; each loops over tiles so the
   // digit histogram is flushed once per workgroup instead of once per tile
-  int per_plane = std::max(1, std::min(ntiles, 768 / std::max(B, 1)));
-  hipLaunchKernelGGL((k_harris<KS, ABL>), dim3(per_plane, B), dim3(256), 0, st, lvl, R, hist, H, W,
-                     tiles_x, ntiles, gk, alpha, scan);
+  int per_plane = std::max(1, std::min(ntiles, 512 / std::max(B, 1)));
+  if ((W & 3) == 0)
+    hipLaunchKernelGGL((k_harris<KS, true, ABL>), dim3(per_plane, B), dim3(256), 0, st, lvl, R, hist, H, W,
+                       tiles_x, ntiles, gk, alpha, scan);
+  else
+    hipLaunchKernelGGL((k_harris<KS, false, ABL>), dim3(per_plane, B), dim3(256), 0, st, lvl, R, hist, H, W,
+                       tiles_x, ntiles, gk, alpha, scan);
 }
 
 void launch_harris(const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
@@ -334,9 +414,6 @@ float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, 
     switch (abl) {
       case 1: launch_ks<7, 1>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
       case 2: launch_ks<7, 2>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
-      case 3: launch_ks<7, 3>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
-      case 4: launch_ks<7, 4>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
-      case 5: launch_ks<7, 5>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
       default: launch_ks<7, 0>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
     }
   };

@@ -94,3 +94,74 @@ class BatchMatcher:
                                  pairs.data_ptr(), P, self.ratio32, out[0].data_ptr(), out[1].data_ptr(),
                                  out[2].data_ptr(), stream)
         return out
+
+
+class BatchPipeline:
+    """Detect + describe + match over a stream of frame batches, `inflight` batches at a
+    time (the throughput path of SURVEY.md §8d; Runner.py:183-191 does the same work one
+    pair at a time on 8 host threads).
+
+    Each in-flight lane owns a context (device workspace + its aux HIP stream), a torch
+    stream, a slot table and match outputs, so batch i+1's pyramid / Harris fill the
+    GPU while batch i's small levels, descriptors and matcher drain.  Batch i runs on
+    lane i % inflight; lanes are reused in order, so a lane's outputs stay valid until
+    `inflight` further batches are submitted (`join()` orders the caller's stream after
+    every lane).
+
+    `hook(slots, B)` runs on the lane's stream between extraction and matching (the halo
+    exchange of a sharded run, distributed.halo_exchange)."""
+
+    def __init__(self, extractor_params: dict | None, ratio_threshold: float, batch: int, H: int, W: int,
+                 pairs, inflight: int = 2, device: int = 0, extra_slots: int = 1):
+        import torch
+        self.torch = torch
+        self.B, self.H, self.W = batch, H, W
+        self.inflight = max(1, int(inflight))
+        self.pairs = pairs
+        dev = torch.device("cuda", device)
+        P = int(pairs.shape[0])
+        self.lanes = []
+        for _ in range(self.inflight):
+            ex = BatchExtractor(extractor_params, device=device)
+            ex.reserve(batch, H, W)
+            m = BatchMatcher(ratio_threshold, device=device, ctx=ex.ctx)
+            slots = SlotTable(torch, batch + extra_slots, ex.cap, dev)
+            view = SlotTable.__new__(SlotTable)
+            view.B, view.cap = batch, ex.cap
+            view.xy, view.desc, view.count = slots.xy[:batch], slots.desc[:batch], slots.count[:batch]
+            mout = (torch.zeros((max(P, 1), max(ex.cap, 1), 2), dtype=torch.int32, device=dev),
+                    torch.zeros((max(P, 1), max(ex.cap, 1)), dtype=torch.float32, device=dev),
+                    torch.zeros((max(P, 1),), dtype=torch.int32, device=dev))
+            self.lanes.append({"ex": ex, "m": m, "slots": slots, "view": view, "mout": mout,
+                               "stream": torch.cuda.Stream(device=dev)})
+        self.cap = self.lanes[0]["ex"].cap
+        self.n = 0
+
+    @property
+    def contexts(self):
+        return [ln["ex"].ctx for ln in self.lanes]
+
+    def submit(self, frames, hook=None):
+        """Enqueue one batch (device [B, H, W] f32 or u8 frames); returns its lane."""
+        torch = self.torch
+        ln = self.lanes[self.n % self.inflight]
+        self.n += 1
+        ln["stream"].wait_stream(torch.cuda.current_stream(frames.device))
+        with torch.cuda.stream(ln["stream"]):
+            ln["ex"].extract(frames, out=ln["view"])
+            if hook is not None:
+                hook(ln["slots"], self.B)
+            ln["m"].match(ln["slots"], self.pairs, out=ln["mout"])
+        return ln
+
+    def join(self):
+        """Make the caller's current stream wait for every lane (no host sync)."""
+        cur = self.torch.cuda.current_stream()
+        for ln in self.lanes:
+            cur.wait_stream(ln["stream"])
+
+    def start(self):
+        """Make every lane wait for the caller's current stream (e.g. after an event)."""
+        cur = self.torch.cuda.current_stream()
+        for ln in self.lanes:
+            ln["stream"].wait_stream(cur)

@@ -265,3 +265,32 @@ def test_1080p_batch_consistency_and_golden():
             assert desc_close(z[f"f{f}_D"], desc[b, :n][perm][::8])
         assert np.array_equal(xy[b, :n], xy[f, :n])
         assert np.array_equal(bits(desc[b, :n]), bits(desc[f, :n]))
+
+
+def test_pipeline_batches_in_flight_match_serial():
+    """pipeline.BatchPipeline (2 batches in flight on separate contexts/streams) gives the
+    same slots and matches as one BatchExtractor/BatchMatcher run per batch."""
+    torch = pytest.importorskip("torch")
+    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, BatchPipeline, consecutive_pairs
+    B, H, W = 4, 270, 480
+    pp = dict(P_OCT, num_interest_points=600)
+    batches = [torch.from_numpy(synth.make_batch_u8(B, H, W, seed=300 + i)).cuda() for i in range(3)]
+    pairs = torch.from_numpy(consecutive_pairs(B)).cuda()
+    pipe = BatchPipeline(pp, 0.85, B, H, W, pairs, inflight=2, extra_slots=0)
+    lanes = [pipe.submit(f) for f in batches]
+    pipe.join()
+    torch.cuda.synchronize()
+    ex = BatchExtractor(pp)
+    m = BatchMatcher(0.85, ctx=ex.ctx)
+    for i in (1, 2):  # lane 0 was reused by batch 2
+        s = ex.extract(batches[i])
+        mm, mc, nm = m.match(s, pairs)
+        torch.cuda.synchronize()
+        ln = lanes[i]
+        assert ln is pipe.lanes[i % 2]
+        for k in ("xy", "desc", "count"):
+            assert torch.equal(getattr(s, k), getattr(ln["slots"], k))
+        assert torch.equal(nm, ln["mout"][2])
+        for p in range(B - 1):
+            k = int(nm[p])
+            assert torch.equal(mm[p, :k], ln["mout"][0][p, :k]) and torch.equal(mc[p, :k], ln["mout"][1][p, :k])
