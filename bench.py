@@ -40,6 +40,10 @@ RATIO = 0.85
 H, W = 1080, 1920
 PEAK_F32_TFLOPS = 157.3   # MI355X FP32 (vector == matrix) dense peak, MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0     # HBM3E spec
+# The matcher's prefilter is split-f16 on the f16 MFMA (dense 2.5 PF): three f16 products
+# (hi*hi, hi*lo, lo*hi) per f32-accurate product, so its algorithmic (GEMM-equivalent)
+# rate is bounded by 2500 / 3 TFLOP/s.
+PEAK_MATCH_TFLOPS = 2500.0 / 3
 
 # algorithmic work: per pixel for the per-level stages, per pair element for
 # the matcher (GEMM-equivalent 2 n1 n2 128 flop)
@@ -100,6 +104,10 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=2,
                     help="frames per host thread in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="disable the live per-stage HIP events")
+    ap.add_argument("--workload", choices=["c2", "c3", "c5"], default="c2",
+                    help="c2 = BASELINE configs[1] (the headline line); c3 = configs[2] (256 frames, all "
+                         "pairs); c5 = configs[4]'s per-GPU share (4K, 5 octaves, k 8000)")
+    ap.add_argument("--frames", type=int, default=256, help="c3: frames in the all-pairs job")
     ap.add_argument("--inflight", type=int, default=2,
                     help="batches in flight (double-buffered contexts / slot tables, pipeline.BatchPipeline)")
     args = ap.parse_args()
@@ -114,6 +122,15 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+
+    if args.workload == "c3":
+        return run_all_pairs(args, torch, dev)
+    if args.workload == "c5":
+        global H, W, P_OCT
+        H, W = 2160, 3840
+        P_OCT = dict(P_OCT, num_interest_points=8000, pyramid_level=5)
+        if args.batch == 32:
+            args.batch = 8
 
     from sfmfromscratch_amd import distributed as D
     from sfmfromscratch_amd import synth
@@ -151,7 +168,7 @@ def main():
         kps = int(counts[:B].sum()) * nsteps
         return {
             "harris": ("mfma", HARRIS_FLOP_PER_PX * px / 1e12, "TFLOP/s", PEAK_F32_TFLOPS),
-            "match": ("mfma", MATCH_FLOP_PER_ELEM * pair_elems / 1e12, "TFLOP/s", PEAK_F32_TFLOPS),
+            "match": ("mfma", MATCH_FLOP_PER_ELEM * pair_elems / 1e12, "TFLOP/s", PEAK_MATCH_TFLOPS),
             "nms": ("hbm", 4.0 * px / 1e9, "GB/s", PEAK_HBM_GBS),          # one read of R
             "pyramid": ("hbm", 4.0 * px_lo * 5 / 1e9, "GB/s", PEAK_HBM_GBS),  # read 4 px, write 1
             "describe": ("hbm", DESC_BYTES_PER_KP * kps / 1e9, "GB/s", PEAK_HBM_GBS),
@@ -250,7 +267,7 @@ def main():
             roof["traffic_note"] = "HBM bytes per launch, rocprofv3 PMC (profiles/pmc_traffic.json)"
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
+    if rank == 0 and world == 1 and args.cpu_sample > 0 and args.workload == "c2":
         v, dt, nt, nf = cpu_baseline(args.cpu_sample)
         cpu = {"value": round(v, 4), "unit": "images/sec", "cores": nt, "kind": "port",
                "sample": f"oracle/sfm_oracle.c (scalar C restatement) on {nt} host threads, each extracting "
@@ -259,7 +276,8 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "images/sec detect+describe+match, 1080p, 1/2/4/8 MI355X",
+            "metric": "images/sec detect+describe+match, 1080p, 1/2/4/8 MI355X" if args.workload == "c2"
+                      else "images/sec detect+describe+match, 4K 5-octave k=8000",
             "value": round(value, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -270,9 +288,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (deterministic integer-generated textured 1080p frames, device-resident f32)",
-            "config": {"workload": "BASELINE configs[1]: 32x 1080p per GPU, ScaleRotInvSIFT 4-level x2 octave "
-                                   "pyramid, k=2500, fw 18, NNRatio 0.85 over consecutive pairs",
+            "data": f"synthetic (deterministic integer-generated textured {H}x{W} frames, device-resident f32)",
+            "config": {"workload": ("BASELINE configs[1]: 32x 1080p per GPU, ScaleRotInvSIFT 4-level x2 octave "
+                                    "pyramid, k=2500, fw 18, NNRatio 0.85 over consecutive pairs")
+                       if args.workload == "c2" else
+                       (f"BASELINE configs[4] per-GPU share: {B}x 4K per step, ScaleRotInvSIFT 5-level x2 "
+                        "octave pyramid, k=8000, fw 18, NNRatio 0.85 over consecutive pairs"),
                        "frames_per_gpu": B, "image": [H, W], "pairs_per_gpu": int(P),
                        "keypoints_mean": float(np.mean(counts[:B])),
                        "matches_mean": float(np.mean(nmatch[nmatch >= 0])) if (nmatch >= 0).any() else 0.0,
@@ -284,6 +305,91 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_all_pairs(args, torch, dev):
+    """BASELINE configs[2]: N (256) device-resident 1080p frames extracted (32 per batch,
+    two batches in flight), then every one of the N(N-1)/2 pairs matched (the matcher's
+    split-f16 MFMA prefilter + exact f32 re-rank).  One step = the whole job."""
+    from sfmfromscratch_amd import synth
+    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, SlotTable, all_pairs
+    N, Bx = args.frames, 32
+    host = np.stack([synth.make_frame_u8(H, W, 1234 + 1000 * (i // 32), i % 32) for i in range(N)])
+    frames = torch.from_numpy(synth.u8_to_gray(host)).to(dev)
+    del host
+    lanes = []
+    for _ in range(max(1, args.inflight)):
+        ex = BatchExtractor(P_OCT, device=dev.index)
+        ex.reserve(Bx, H, W)
+        lanes.append((ex, torch.cuda.Stream(device=dev)))
+    cap = lanes[0][0].cap
+    slots = SlotTable(torch, N, cap, dev)
+    matcher = BatchMatcher(RATIO, device=dev.index, ctx=lanes[0][0].ctx)
+    pairs_np = all_pairs(N)
+    pairs = torch.from_numpy(pairs_np).to(dev)
+    P = len(pairs_np)
+    CH = 4096  # pairs per matcher launch
+    out = (torch.zeros((P, cap, 2), dtype=torch.int32, device=dev),
+           torch.zeros((P, cap), dtype=torch.float32, device=dev),
+           torch.zeros((P,), dtype=torch.int32, device=dev))
+
+    class View:
+        pass
+
+    def step():
+        cur = torch.cuda.current_stream()
+        for b0 in range(0, N, Bx):
+            ex, stm = lanes[(b0 // Bx) % len(lanes)]
+            stm.wait_stream(cur)
+            v = View()
+            v.xy, v.desc, v.count = slots.xy[b0:b0 + Bx], slots.desc[b0:b0 + Bx], slots.count[b0:b0 + Bx]
+            with torch.cuda.stream(stm):
+                ex.extract(frames[b0:b0 + Bx], out=v)
+        for _, stm in lanes:
+            cur.wait_stream(stm)
+        for a in range(0, P, CH):
+            matcher.match(slots, pairs[a:a + CH], out=(out[0][a:a + CH], out[1][a:a + CH], out[2][a:a + CH]))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx = matcher.ctx
+    ctx.profile_enable(True)
+    ctx.profile_stages(["match"])
+    ctx.profile_read(reset=True)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    elapsed = max(time.perf_counter() - t0, ev0.elapsed_time(ev1) / 1e3)
+    prof = ctx.profile_read(reset=True)
+    ctx.profile_enable(False)
+    counts = slots.count.cpu().numpy().astype(np.int64)
+    nm = out[2].cpu().numpy()
+    elems = int(sum(counts[i] * counts[j] for i, j in pairs_np)) * 128 * args.steps
+    ms, n = prof.get("match", (0.0, 0))
+    ach = MATCH_FLOP_PER_ELEM * elems / 1e12 / (ms / 1e3) if ms else None
+    print(json.dumps({
+        "metric": "images/sec detect+describe+match, 1080p, all pairs (BASELINE configs[2])",
+        "value": round(N * args.steps / elapsed, 3), "unit": "images/sec", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (deterministic integer-generated textured 1080p frames, device-resident f32)",
+        "config": {"workload": f"BASELINE configs[2]: {N}x 1080p, ScaleRotInvSIFT 4-level x2 octave pyramid, "
+                               f"k=2500, NNRatio 0.85 over all {P} pairs",
+                   "frames": N, "pairs": P, "pairs_per_sec": round(P * args.steps / elapsed, 1),
+                   "keypoints_mean": float(counts.mean()), "matches_mean": float(nm[nm >= 0].mean()),
+                   "parallelism": "single GPU"},
+        "roofline": {"kernel": KERNELS["match"], "stage": "match", "bound": "mfma",
+                     "achieved": round(ach, 3) if ach else None, "peak": round(PEAK_MATCH_TFLOPS, 1),
+                     "unit": "TFLOP/s", "frac": round(ach / PEAK_MATCH_TFLOPS, 4) if ach else None, "traffic": None,
+                     "avg_launch_ms": round(ms / max(n, 1), 4), "launches": n,
+                     "note": "GEMM-equivalent 2*n1*n2*128 flop per pair (SURVEY.md §8d) against the split-f16 "
+                             "MFMA bound 2500/3 TFLOP/s"},
+        "cpu_baseline": None}), flush=True)
 
 
 if __name__ == "__main__":

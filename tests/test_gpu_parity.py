@@ -288,9 +288,63 @@ def test_pipeline_batches_in_flight_match_serial():
         torch.cuda.synchronize()
         ln = lanes[i]
         assert ln is pipe.lanes[i % 2]
-        for k in ("xy", "desc", "count"):
-            assert torch.equal(getattr(s, k), getattr(ln["slots"], k))
+        assert torch.equal(s.count, ln["slots"].count)
+        for b, n in enumerate(s.count.tolist()):  # rows past the count are stale in a reused lane
+            assert torch.equal(s.xy[b, :n], ln["slots"].xy[b, :n])
+            assert torch.equal(s.desc[b, :n], ln["slots"].desc[b, :n])
         assert torch.equal(nm, ln["mout"][2])
         for p in range(B - 1):
             k = int(nm[p])
             assert torch.equal(mm[p, :k], ln["mout"][0][p, :k]) and torch.equal(mc[p, :k], ln["mout"][1][p, :k])
+
+
+P_4K = dict(P_MAIN, num_interest_points=8000, pyramid_level=5, pyramid_scale_factor=2)
+
+
+def test_4k_five_octaves_k8000_vs_oracle():
+    """BASELINE configs[4] at full size: 4K frames, 5-level x2 pyramid, k = 8000
+    (1600 per level).  Keypoints + descriptors bit-identical to the oracle, and the
+    ~7-8k x 7-8k pair matched identically."""
+    torch = pytest.importorskip("torch")
+    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, consecutive_pairs
+    H, W = 2160, 3840
+    u8 = synth.make_batch_u8(2, H, W, seed=4321)
+    ex = BatchExtractor(P_4K)
+    s = ex.extract(torch.from_numpy(u8).cuda())
+    pairs = torch.from_numpy(consecutive_pairs(2)).cuda()
+    mm, mc, nm = BatchMatcher(0.85, ctx=ex.ctx).match(s, pairs)
+    torch.cuda.synchronize()
+    counts = s.count.cpu().numpy()
+    xy = s.xy.cpu().numpy()
+    desc = s.desc.cpu().numpy()
+    assert counts.min() > 5000, counts
+    OX, OY, OD, _ = O.extract(synth.u8_to_gray(u8[0]), P_4K)
+    n = counts[0]
+    assert n == len(OX)
+    assert np.array_equal(xy[0, :n, 0], OX) and np.array_equal(xy[0, :n, 1], OY)
+    assert np.array_equal(bits(desc[0, :n]), bits(OD))
+    om, oc = O.match(desc[0, :counts[0]], desc[1, :counts[1]], 0.85)
+    k = int(nm[0])
+    assert k > 1000
+    assert_matches_equal(om, oc, mm[0, :k].cpu().numpy(), mc[0, :k].cpu().numpy())
+
+
+def test_all_pairs_schedule_vs_oracle():
+    """All-pairs matching (BASELINE configs[2] schedule) over one slot table: every
+    upper-triangle pair equals the oracle's matcher on the same descriptors."""
+    torch = pytest.importorskip("torch")
+    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, all_pairs
+    B, H, W = 6, 270, 480
+    pp = dict(P_OCT, num_interest_points=800)
+    ex = BatchExtractor(pp)
+    s = ex.extract(torch.from_numpy(synth.make_batch_u8(B, H, W, seed=91)).cuda())
+    pairs_np = all_pairs(B)
+    mm, mc, nm = BatchMatcher(0.85, ctx=ex.ctx).match(s, torch.from_numpy(pairs_np).cuda())
+    torch.cuda.synchronize()
+    counts = s.count.cpu().numpy()
+    desc = s.desc.cpu().numpy()
+    assert len(pairs_np) == B * (B - 1) // 2
+    for p, (i, j) in enumerate(pairs_np):
+        om, oc = O.match(desc[i, :counts[i]], desc[j, :counts[j]], 0.85)
+        k = int(nm[p])
+        assert_matches_equal(om, oc, mm[p, :k].cpu().numpy(), mc[p, :k].cpu().numpy())
