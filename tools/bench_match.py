@@ -12,18 +12,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--allpairs", action="store_true", help="all B(B-1)/2 pairs instead of consecutive")
     args = ap.parse_args()
     import numpy as np
     import torch
     from sfmfromscratch_amd import synth
-    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, consecutive_pairs
+    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, all_pairs, consecutive_pairs
     P_OCT = {"num_interest_points": 2500, "ksize": 3, "gaussian_size": 7, "sigma": 6, "alpha": 0.05,
              "feature_width": 18, "pyramid_level": 4, "pyramid_scale_factor": 2}
     B = args.batch
     ex = BatchExtractor(P_OCT)
     u8 = np.stack([synth.make_frame_u8(1080, 1920, 1234, i) for i in range(B)])
     slots = ex.extract(torch.from_numpy(u8).cuda())
-    pairs = torch.from_numpy(consecutive_pairs(B)).cuda()
+    pairs = torch.from_numpy(all_pairs(B) if args.allpairs else consecutive_pairs(B)).cuda()
     m = BatchMatcher(0.85, ctx=ex.ctx)
     out = m.match(slots, pairs)
     torch.cuda.synchronize()
@@ -34,7 +35,7 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.iters
-    print(f"match {B - 1} pairs: {ms:.3f} ms per call, keypoints mean {slots.count.float().mean().item():.0f}, "
+    print(f"match {pairs.shape[0]} pairs: {ms * 1e3 / pairs.shape[0]:.2f} us/pair, {ms:.3f} ms per call, keypoints mean {slots.count.float().mean().item():.0f}, "
           f"matches mean {out[2].float().mean().item():.0f}")
 
 
