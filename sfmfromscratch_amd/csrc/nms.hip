@@ -109,26 +109,65 @@ __global__ void __launch_bounds__(256) k_nms_tile(const float* __restrict__ R,
     if (tile + (int)gridDim.x < ntiles) prefetch(tile + gridDim.x);
     uint32_t flags = 0;
     float vals[16];
+    // pixel q of this thread: KH == 1 -> 4 x 4 block (rows 4rg + q/4, columns 4cg + q%4);
+    // otherwise 8 columns x rows tid/8 and tid/8 + 32
+    const int cg = tid & 15, rg = tid >> 4;
+    auto pix_r = [&](int q) { return KH == 1 ? 4 * rg + (q >> 2) : (tid >> 3) + 32 * (q >> 3); };
+    auto pix_c = [&](int q) { return KH == 1 ? 4 * cg + (q & 3) : c0 + (q & 7); };
+    if constexpr (KH == 1) {
+      // separable 3 x 3 max from 16-B LDS reads (a 16-lane group reads 16 distinct
+      // chunks of one row): per input row the horizontal max3 of the 4 columns, then the
+      // vertical max3; max is exact, so v == max <=> no cell of the window is larger
+      float hm[6][4], ctr[4][4];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int r = (tid >> 3) + 32 * (q >> 3), c = c0 + (q & 7);
-      const float v = s_t[r + KH][4 + c];
-      vals[q] = v;
-      const bool inside = ty0 + r < H && tx0 + c < W;
-      bool pred = false;
-      if (inside && (MODE == 1 || fkey(v) >= tnms)) {
-        if (MODE == 1 && v < med) {
-          pred = (v == 0.0f);  // R_maxpool[R < median] = 0 (:92)
-        } else {
-          bool ismax = true;
+      for (int i = 0; i < 6; ++i) {
+        const float* row = &s_t[4 * rg + i][4 * cg];
+        const float4 a = *reinterpret_cast<const float4*>(row);
+        const float4 bq = *reinterpret_cast<const float4*>(row + 4);
+        const float cx = row[8];
+        const float x[6] = {a.w, bq.x, bq.y, bq.z, bq.w, cx};
 #pragma unroll
-          for (int dy = -KH; dy <= KH; ++dy)
-#pragma unroll
-            for (int dx = -KH; dx <= KH; ++dx) ismax &= !(s_t[r + KH + dy][4 + c + dx] > v);
-          pred = ismax;
+        for (int e = 0; e < 4; ++e) hm[i][e] = fmaxf(fmaxf(x[e], x[e + 1]), x[e + 2]);
+        if (i >= 1 && i <= 4) {
+          ctr[i - 1][0] = bq.x; ctr[i - 1][1] = bq.y; ctr[i - 1][2] = bq.z; ctr[i - 1][3] = bq.w;
         }
       }
-      flags |= pred ? (1u << q) : 0u;
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int q = 4 * o + e;
+          const float v = ctr[o][e];
+          vals[q] = v;
+          const float m = fmaxf(fmaxf(hm[o][e], hm[o + 1][e]), hm[o + 2][e]);
+          const bool inside = ty0 + 4 * rg + o < H && tx0 + 4 * cg + e < W;
+          bool pred;
+          if (MODE == 0) pred = fkey(v) >= tnms && v == m;
+          else pred = (v < med) ? (v == 0.0f) : (v == m);  // R_maxpool[R < median] = 0 (:92)
+          flags |= (inside && pred) ? (1u << q) : 0u;
+        }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int r = pix_r(q), c = pix_c(q);
+        const float v = s_t[r + KH][4 + c];
+        vals[q] = v;
+        const bool inside = ty0 + r < H && tx0 + c < W;
+        bool pred = false;
+        if (inside && (MODE == 1 || fkey(v) >= tnms)) {
+          if (MODE == 1 && v < med) {
+            pred = (v == 0.0f);  // R_maxpool[R < median] = 0 (:92)
+          } else {
+            bool ismax = true;
+#pragma unroll
+            for (int dy = -KH; dy <= KH; ++dy)
+#pragma unroll
+              for (int dx = -KH; dx <= KH; ++dx) ismax &= !(s_t[r + KH + dy][4 + c + dx] > v);
+            pred = ismax;
+          }
+        }
+        flags |= pred ? (1u << q) : 0u;
+      }
     }
     if (__syncthreads_or(flags != 0)) {
       const int64_t slot = block_append(&cand_count[(int64_t)b * kCounterStride], (uint32_t)__popc(flags),
@@ -137,7 +176,7 @@ __global__ void __launch_bounds__(256) k_nms_tile(const float* __restrict__ R,
 #pragma unroll
       for (int q = 0; q < 16; ++q)
         if (flags & (1u << q)) {
-          const int r = (tid >> 3) + 32 * (q >> 3), c = c0 + (q & 7);
+          const int r = pix_r(q), c = pix_c(q);
           *out++ = ((uint64_t)(~fkey(vals[q])) << 32) | (uint32_t)((ty0 + r) * W + tx0 + c);
         }
     }
