@@ -130,6 +130,19 @@ int32_t sfm_extract(sfm_ctx* ctx, const float* img, int32_t H, int32_t W, int64_
 int32_t sfm_match(sfm_ctx* ctx, const float* d1, int64_t n1, const float* d2, int64_t n2,
                   float ratio, int64_t* matches, float* conf, int64_t cap, int64_t* k_out);
 
+/*
+ * Frame ingest of FeatureRunner (Runner.py:33-46): a decoded RGB frame ([H][W][3] uint8,
+ * what _load_image reads, Runner.py:551-563) -> PIL BICUBIC resize to W2 x H2
+ * (_PIL_resize, Runner.py:37-42,481-493; Pillow's 8-bit fixed-point resampler, bit
+ * exact) -> /255 -> _rgb2gray (Runner.py:467-478) -> [H2][W2] float32, the image the
+ * extractor classes take.  Host pointers; synchronous.
+ */
+int32_t sfm_ingest_rgb(sfm_ctx* ctx, const uint8_t* rgb, int32_t H, int32_t W, int32_t H2, int32_t W2,
+                       float* gray);
+
+/* (int(H * scale), int(W * scale)) — the PIL target size of Runner.py:37-42. */
+int32_t sfm_resize_dims(int32_t H, int32_t W, double scale, int32_t* H2, int32_t* W2);
+
 /* ---------------- device-resident batch API (throughput path) ----------------
  * All pointers are device pointers on the context's device; `stream` is the
  * hipStream_t the work is enqueued on, exactly as given (NULL = HIP's null stream, as
@@ -145,6 +158,10 @@ int32_t sfm_match(sfm_ctx* ctx, const float* d1, int64_t n1, const float* d2, in
  *   count [B] int32
  */
 int32_t sfm_reserve(sfm_ctx* ctx, int32_t B, int32_t H, int32_t W);
+
+/* sfm_ingest_rgb for B frames: rgb [B][H][W][3] uint8 -> gray [B][H2][W2] float32. */
+int32_t sfm_ingest_rgb_dev(sfm_ctx* ctx, const uint8_t* rgb, int32_t B, int32_t H, int32_t W,
+                           int32_t H2, int32_t W2, float* gray, void* stream);
 
 /* Extract B images of identical size H x W stored contiguously ([B][H][W] float32). */
 int32_t sfm_extract_batch_dev(sfm_ctx* ctx, const float* imgs, int32_t B, int32_t H, int32_t W,
@@ -198,8 +215,7 @@ int32_t sfm_debug_harris(int32_t device, const float* gauss, int32_t gs, double 
                          float* median_out, int64_t* ncand_out);
 
 /* Mean time (ms) of one fused Harris launch on synthetic planes, ablation variant abl
- * (0 full, 1 no digit histogram, 2 no window sums, 3 no Sobel/products, 4 image load +
- * R store only, 5 R store only). */
+ * (0 full, 1 no digit histogram, 2 window sums over the first tap row only). */
 float sfm_debug_time_harris(int32_t device, int32_t abl, int32_t B, int32_t H, int32_t W,
                             int32_t iters);
 

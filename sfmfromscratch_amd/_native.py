@@ -41,6 +41,11 @@ SIGNATURES = {
     "sfm_match": (ctypes.c_int32, [_vp, _fp, ctypes.c_int64, _fp, ctypes.c_int64, ctypes.c_float, _i64p, _fp,
                                    ctypes.c_int64, _i64p]),
     "sfm_reserve": (ctypes.c_int32, [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "sfm_ingest_rgb": (ctypes.c_int32, [_vp, _u8p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                        _fp]),
+    "sfm_resize_dims": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_double, _i32p, _i32p]),
+    "sfm_ingest_rgb_dev": (ctypes.c_int32, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
     "sfm_extract_batch_dev": (ctypes.c_int32, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp, _vp,
                                                _vp, ctypes.c_int64, _vp]),
     "sfm_extract_batch_u8_dev": (ctypes.c_int32, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp,
@@ -129,6 +134,15 @@ def _params_key(p: SfmParams) -> bytes:
     return bytes(memoryview(p))
 
 
+def resize_dims(H: int, W: int, scale: float = 0.5) -> tuple[int, int]:
+    """(int(H * scale), int(W * scale)), the PIL target size of Runner.py:37-42."""
+    h2, w2 = ctypes.c_int32(0), ctypes.c_int32(0)
+    rc = load_library().sfm_resize_dims(H, W, ctypes.c_double(scale), ctypes.byref(h2), ctypes.byref(w2))
+    if rc != _abi.SFM_OK:
+        raise ValueError(f"bad resize: {H}x{W} * {scale}")
+    return int(h2.value), int(w2.value)
+
+
 class Context:
     """One sfm_ctx (device workspace + HIP stream) for a fixed parameter set."""
 
@@ -199,7 +213,25 @@ class Context:
         check(rc, self.handle)
         return m[:k.value], c[:k.value]
 
+    def ingest_rgb(self, rgb: np.ndarray, scale: float = 0.5) -> np.ndarray:
+        """FeatureRunner's ingest (Runner.py:33-46) of one decoded [H, W, 3] uint8 RGB frame:
+        PIL BICUBIC resize to int(shape * scale), /255, _rgb2gray -> [H2, W2] float32."""
+        rgb = np.ascontiguousarray(rgb)
+        if rgb.dtype != np.uint8 or rgb.ndim != 3 or rgb.shape[2] != 3:
+            raise ValueError("ingest_rgb expects an [H, W, 3] uint8 RGB frame")
+        H, W = rgb.shape[:2]
+        H2, W2 = resize_dims(H, W, scale)
+        out = np.empty((H2, W2), np.float32)
+        check(self.lib.sfm_ingest_rgb(self.handle, rgb.ctypes.data_as(_u8p), H, W, H2, W2, out.ctypes.data_as(_fp)),
+              self.handle)
+        return out
+
     # -------- device-pointer API (throughput path; pointers are ints) --------
+    def ingest_rgb_dev(self, rgb_ptr: int, B: int, H: int, W: int, H2: int, W2: int, gray_ptr: int,
+                       stream: int = 0):
+        check(self.lib.sfm_ingest_rgb_dev(self.handle, rgb_ptr, B, H, W, H2, W2, gray_ptr, stream or None),
+              self.handle)
+
     def reserve(self, B: int, H: int, W: int):
         check(self.lib.sfm_reserve(self.handle, B, H, W), self.handle)
 

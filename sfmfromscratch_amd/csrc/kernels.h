@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "common.h"
 
 namespace sfm {
@@ -130,6 +132,13 @@ struct KpList {
 
 // pyramid.hip
 void launch_u8_to_f32(const uint8_t* src, float* dst, int64_t n, hipStream_t st);
+
+// ingest.hip: PIL BICUBIC resize of [B][H][W][3] u8 RGB to H2 x W2 + /255 + _rgb2gray
+// (Runner.py:33-46) -> [B][H2][W2] float32; tmp holds [B][H][W2][3] u8.  Tables from
+// build_resample_table (host, Pillow's double-precision taps in 22-bit fixed point).
+int build_resample_table(int in, int out, std::vector<int32_t>& tab);
+void launch_ingest_rgb(const uint8_t* rgb, uint8_t* tmp, float* gray, const int32_t* tab_h, int ks_h,
+                       const int32_t* tab_v, int ks_v, int B, int H, int W, int H2, int W2, hipStream_t st);
 void launch_resize(const float* src, int sh, int sw, float* dst, int dh, int dw, int B,
                    hipStream_t st);
 

@@ -53,6 +53,10 @@ struct sfm_ctx {
       d_kpx, d_kpy, d_kpc, d_lc, d_xy, d_desc, d_conf, d_count, d_u8;
   DevBuf m_desc, m_count, m_pairs, m_descT, m_rows, m_matches, m_conf, m_nmatch;
   DevBuf m_hi, m_lo, m_norm2, m_rnorm, m_imgmax;
+  // ingest (sfm_ingest_rgb*): resample tables for the cached (W -> W2, H -> H2) and the
+  // RGB temp of the horizontal pass; host staging for the host-pointer variant
+  DevBuf i_tab_h, i_tab_v, i_tmp, i_rgb, i_gray;
+  int i_w = -1, i_w2 = -1, i_h = -1, i_h2 = -1, i_ksh = 0, i_ksv = 0;
   bool match_direct = false;  // SFMFEAT_MATCH_DIRECT=1: all-pairs exact VALU kernel (A/B checks)
   bool exact_select = false;
   bool serial = false;        // SFMFEAT_SERIAL=1: no aux-stream overlap (diagnostic timings)  // SFMFEAT_SELECT=exact: every plane takes the exact-median path
@@ -502,7 +506,8 @@ int32_t sfm_ctx_destroy(sfm_ctx* c) {
                     &c->d_counts, &c->d_cand, &c->d_scratch, &c->d_kpx, &c->d_kpy, &c->d_kpc, &c->d_lc,
                     &c->d_xy, &c->d_desc, &c->d_conf, &c->d_count, &c->d_u8, &c->m_desc, &c->m_count, &c->m_pairs,
                     &c->m_descT, &c->m_rows, &c->m_matches, &c->m_conf, &c->m_nmatch,
-                    &c->m_hi, &c->m_lo, &c->m_norm2, &c->m_rnorm, &c->m_imgmax};
+                    &c->m_hi, &c->m_lo, &c->m_norm2, &c->m_rnorm, &c->m_imgmax,
+                    &c->i_tab_h, &c->i_tab_v, &c->i_tmp, &c->i_rgb, &c->i_gray};
   for (DevBuf* b : bufs) free_buf(*b);
   for (auto& e : c->prof_pending) {
     (void)hipEventDestroy(e.second.first);
@@ -542,6 +547,67 @@ int32_t sfm_extract_batch_u8_dev(sfm_ctx* c, const uint8_t* imgs, int32_t B, int
   if (rc) return rc;
   launch_u8_to_f32(imgs, as<float>(c->d_img0), (int64_t)B * H * W, st);
   return extract_impl(c, as<float>(c->d_img0), B, H, W, xy, desc, nullptr, count, cap, st);
+}
+
+int32_t sfm_resize_dims(int32_t H, int32_t W, double scale, int32_t* H2, int32_t* W2) {
+  if (!H2 || !W2 || H < 1 || W < 1 || !(scale > 0.0)) return SFM_EINVAL;
+  const double h = (double)H * scale, w = (double)W * scale;  // int(shape * scale_factor)
+  if (h < 1.0 || w < 1.0 || h > 65535.0 || w > 65535.0) return SFM_EINVAL;
+  *H2 = (int32_t)h;
+  *W2 = (int32_t)w;
+  return SFM_OK;
+}
+
+namespace {
+int ingest_impl(sfm_ctx* c, const uint8_t* rgb, int B, int H, int W, int H2, int W2, float* gray,
+                hipStream_t st) {
+  int rc;
+  if (c->i_w != W || c->i_w2 != W2) {
+    std::vector<int32_t> t;
+    c->i_ksh = build_resample_table(W, W2, t);
+    if ((rc = ensure(c, c->i_tab_h, t.size() * 4))) return rc;
+    HIPCHK(c, hipMemcpy(c->i_tab_h.p, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+    c->i_w = W;
+    c->i_w2 = W2;
+  }
+  if (c->i_h != H || c->i_h2 != H2) {
+    std::vector<int32_t> t;
+    c->i_ksv = build_resample_table(H, H2, t);
+    if ((rc = ensure(c, c->i_tab_v, t.size() * 4))) return rc;
+    HIPCHK(c, hipMemcpy(c->i_tab_v.p, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+    c->i_h = H;
+    c->i_h2 = H2;
+  }
+  if ((rc = ensure(c, c->i_tmp, (size_t)B * H * W2 * 3))) return rc;
+  launch_ingest_rgb(rgb, as<uint8_t>(c->i_tmp), gray, as<int32_t>(c->i_tab_h), c->i_ksh, as<int32_t>(c->i_tab_v),
+                    c->i_ksv, B, H, W, H2, W2, st);
+  HIPCHK(c, hipGetLastError());
+  return SFM_OK;
+}
+}  // namespace
+
+int32_t sfm_ingest_rgb_dev(sfm_ctx* c, const uint8_t* rgb, int32_t B, int32_t H, int32_t W, int32_t H2,
+                           int32_t W2, float* gray, void* stream) {
+  if (!c || !rgb || !gray || B < 1 || H < 1 || W < 1 || H2 < 1 || W2 < 1 || H2 > 65535 || W2 > 65535)
+    return SFM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  return ingest_impl(c, rgb, B, H, W, H2, W2, gray, (hipStream_t)stream);
+}
+
+int32_t sfm_ingest_rgb(sfm_ctx* c, const uint8_t* rgb, int32_t H, int32_t W, int32_t H2, int32_t W2,
+                       float* gray) {
+  if (!c || !rgb || !gray || H < 1 || W < 1 || H2 < 1 || W2 < 1 || H2 > 65535 || W2 > 65535)
+    return SFM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure(c, c->i_rgb, (size_t)H * W * 3))) return rc;
+  if ((rc = ensure(c, c->i_gray, (size_t)H2 * W2 * 4))) return rc;
+  hipStream_t st = c->stream;
+  HIPCHK(c, hipMemcpyAsync(c->i_rgb.p, rgb, (size_t)H * W * 3, hipMemcpyHostToDevice, st));
+  if ((rc = ingest_impl(c, as<uint8_t>(c->i_rgb), 1, H, W, H2, W2, as<float>(c->i_gray), st))) return rc;
+  HIPCHK(c, hipMemcpyAsync(gray, c->i_gray.p, (size_t)H2 * W2 * 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  return SFM_OK;
 }
 
 int32_t sfm_extract(sfm_ctx* c, const float* img, int32_t H, int32_t W, int64_t row_stride, int64_t* X,

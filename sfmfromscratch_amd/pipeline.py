@@ -35,6 +35,24 @@ class SlotTable:
         self.count = torch.zeros((B,), dtype=torch.int32, device=device)
 
 
+def ingest_rgb(ctx: Context, rgb, scale: float = 0.5, out=None):
+    """Device ingest of a batch of decoded RGB frames (FeatureRunner, Runner.py:33-46):
+    rgb [B, H, W, 3] uint8 cuda tensor -> [B, int(H*scale), int(W*scale)] float32 gray
+    (PIL BICUBIC resize, /255, _rgb2gray), enqueued on torch's current stream."""
+    import torch
+    from ._native import resize_dims
+    assert rgb.is_cuda and rgb.dtype == torch.uint8 and rgb.dim() == 4 and rgb.shape[3] == 3
+    rgb = rgb.contiguous()
+    B, H, W, _ = rgb.shape
+    H2, W2 = resize_dims(H, W, scale)
+    if out is None:
+        out = torch.empty((B, H2, W2), dtype=torch.float32, device=rgb.device)
+    assert out.shape == (B, H2, W2) and out.dtype == torch.float32 and out.is_contiguous()
+    stream = torch.cuda.current_stream(rgb.device).cuda_stream
+    ctx.ingest_rgb_dev(rgb.data_ptr(), B, H, W, H2, W2, out.data_ptr(), stream)
+    return out
+
+
 class BatchExtractor:
     """Batched ScaleRotInvSIFT / NaiveSIFT extraction on device-resident frames."""
 

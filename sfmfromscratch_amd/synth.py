@@ -80,6 +80,13 @@ def make_frame_u8(H: int, W: int, seed: int = 1234, index: int = 0) -> np.ndarra
     return img.astype(np.uint8)
 
 
+def make_frame_rgb_u8(H: int, W: int, seed: int = 1234, index: int = 0) -> np.ndarray:
+    """Frame `index` as an H x W x 3 uint8 RGB array (the decoded JPEG the reference's
+    _load_image reads, Runner.py:551-563): one scene per channel (seeds seed, seed+1,
+    seed+2), so the channels are correlated in motion but differ in content."""
+    return np.stack([make_frame_u8(H, W, seed + c, index) for c in range(3)], axis=-1)
+
+
 def u8_to_gray(u8: np.ndarray) -> np.ndarray:
     """value / 255 in float32 (Runner.py:521 `_im2single`-style conversion)."""
     return u8.astype(np.float32) / np.float32(255.0)

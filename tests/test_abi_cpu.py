@@ -120,3 +120,12 @@ def test_product_fails_loudly_without_device_or_library(monkeypatch):
         ScaleRotInvSIFT(np.zeros((64, 64), np.float32), {})
     with pytest.raises(_native.NativeLibraryMissing):
         _native.load_library("/nonexistent/libsfmfeat.so")
+
+
+def test_resize_dims_like_runner():
+    """sfm_resize_dims == (int(H * s), int(W * s)) of Runner.py:37-42 (host arithmetic only)."""
+    from sfmfromscratch_amd._native import resize_dims
+    for H, W, s in [(2160, 3840, 0.5), (481, 641, 0.5), (90, 60, 0.75), (7, 9, 0.3), (100, 100, 1.7)]:
+        assert resize_dims(H, W, s) == (int(H * s), int(W * s))
+    with pytest.raises(ValueError):
+        resize_dims(1, 1, 0.5)

@@ -206,6 +206,31 @@ def gen_match():
     save("match.npz", ncases=np.array(len(cases)), **out)
 
 
+def gen_ingest():
+    """FeatureRunner's ingest (Runner.py:33-46) run by the reference's own helpers on
+    synthetic decoded RGB frames: _load_image's u8 -> float32 / 255 (:551-563),
+    _PIL_resize to (int(W*s), int(H*s)) (:37-42, :481-493), _rgb2gray (:467-478).
+    Small cases keep the whole gray output; the 4K -> 1080p case keeps its SHA-256."""
+    import Runner  # the reference harness (imports PIL, matplotlib and the cv2 stand-in)
+    cases = [(240, 320, 11, 0, 0.5), (241, 479, 12, 1, 0.5), (64, 97, 13, 2, 0.5), (90, 60, 14, 0, 0.75),
+             (2160, 3840, 15, 0, 0.5)]
+    out = {"ncases": np.int64(len(cases))}
+    for i, (H, W, seed, idx, s) in enumerate(cases):
+        rgb = synth.make_frame_rgb_u8(H, W, seed, idx)
+        img = rgb.astype(np.float64).astype(np.float32) / 255           # _load_image / _im2single
+        size = (int(img.shape[1] * s), int(img.shape[0] * s))
+        g = Runner._rgb2gray(Runner._PIL_resize(img, size))
+        assert g.dtype == np.float32
+        out[f"c{i}_meta"] = np.array([H, W, seed, idx], np.int64)
+        out[f"c{i}_scale"] = np.float64(s)
+        out[f"c{i}_sha_in"] = np.array(synth.frame_sha256(rgb))
+        out[f"c{i}_sha_out"] = np.array(synth.frame_sha256(g))
+        out[f"c{i}_shape"] = np.array(g.shape, np.int64)
+        if H * W <= 240 * 480:
+            out[f"c{i}_gray"] = g
+    save("ingest.npz", **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-1080p", action="store_true")
@@ -219,6 +244,7 @@ def main():
         "detect": gen_detect,
         "descriptors": gen_descriptors,
         "match": gen_match,
+        "ingest": gen_ingest,
         "small": lambda: (gen_extract("extract_small_scalerot.npz", 150, 200, 21, P_OCT, "scalerot"),
                           gen_extract("extract_small_pmain.npz", 151, 203, 22, P_MAIN, "scalerot"),
                           gen_extract("extract_small_naive.npz", 150, 200, 23, {"num_interest_points": 500},
