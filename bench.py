@@ -108,6 +108,9 @@ def main():
                     help="c2 = BASELINE configs[1] (the headline line); c3 = configs[2] (256 frames, all "
                          "pairs); c5 = configs[4]'s per-GPU share (4K, 5 octaves, k 8000)")
     ap.add_argument("--frames", type=int, default=256, help="c3: frames in the all-pairs job")
+    ap.add_argument("--rgb-ingest", action="store_true",
+                    help="c2: frames resident as decoded 2x-size RGB (3840x2160x3 u8); each step first runs "
+                         "FeatureRunner's ingest on the device (PIL BICUBIC x0.5 + _rgb2gray, Runner.py:33-46)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="batches in flight (double-buffered contexts / slot tables, pipeline.BatchPipeline)")
     args = ap.parse_args()
@@ -138,9 +141,16 @@ def main():
 
     B = args.batch
     # device-resident float32 frames of this rank's shard of the global sequence
-    frames_u8 = np.stack([synth.make_frame_u8(H, W, 1234, rank * B + i) for i in range(B)])
-    frames = torch.from_numpy(synth.u8_to_gray(frames_u8)).to(dev)
-    del frames_u8
+    rgb = None
+    if args.rgb_ingest:  # decoded RGB at twice the size; the gray frames are made on the device
+        uniq = [synth.make_frame_rgb_u8(2 * H, 2 * W, 1234, rank * B + i) for i in range(min(B, 8))]
+        rgb = torch.from_numpy(np.stack([uniq[i % len(uniq)] for i in range(B)])).to(dev)
+        del uniq
+        frames = torch.empty((B, H, W), dtype=torch.float32, device=dev)
+    else:
+        frames_u8 = np.stack([synth.make_frame_u8(H, W, 1234, rank * B + i) for i in range(B)])
+        frames = torch.from_numpy(synth.u8_to_gray(frames_u8)).to(dev)
+        del frames_u8
     pairs_np = D.local_consecutive_pairs(B, rank, world)
     pairs = torch.from_numpy(pairs_np).to(dev)
     P = pairs.shape[0]
@@ -151,8 +161,20 @@ def main():
     def halo(slots, n):
         D.halo_exchange(dist, slots, n, rank, world)
 
-    def step():
-        pipe.submit(frames, hook=halo)
+    if rgb is not None:
+        from sfmfromscratch_amd.pipeline import ingest_rgb
+        lane_frames = [torch.empty_like(frames) for _ in pipe.lanes]
+
+        def step():  # ingest on the lane's stream, then extract + match there
+            ln = pipe.lanes[pipe.n % pipe.inflight]
+            f = lane_frames[pipe.n % pipe.inflight]
+            ln["stream"].wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(ln["stream"]):
+                ingest_rgb(ln["ex"].ctx, rgb, 0.5, out=f)
+                pipe.submit(f, hook=halo)
+    else:
+        def step():
+            pipe.submit(frames, hook=halo)
 
     for _ in range(args.warmup):
         step()
@@ -290,7 +312,8 @@ def main():
             "dtype": "f32",
             "data": f"synthetic (deterministic integer-generated textured {H}x{W} frames, device-resident f32)",
             "config": {"workload": ("BASELINE configs[1]: 32x 1080p per GPU, ScaleRotInvSIFT 4-level x2 octave "
-                                    "pyramid, k=2500, fw 18, NNRatio 0.85 over consecutive pairs")
+                                    "pyramid, k=2500, fw 18, NNRatio 0.85 over consecutive pairs"
+                                    + (" (+ device ingest from 3840x2160 RGB)" if args.rgb_ingest else ""))
                        if args.workload == "c2" else
                        (f"BASELINE configs[4] per-GPU share: {B}x 4K per step, ScaleRotInvSIFT 5-level x2 "
                         "octave pyramid, k=8000, fw 18, NNRatio 0.85 over consecutive pairs"),

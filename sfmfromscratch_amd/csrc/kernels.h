@@ -137,8 +137,12 @@ void launch_u8_to_f32(const uint8_t* src, float* dst, int64_t n, hipStream_t st)
 // (Runner.py:33-46) -> [B][H2][W2] float32; tmp holds [B][H][W2][3] u8.  Tables from
 // build_resample_table (host, Pillow's double-precision taps in 22-bit fixed point).
 int build_resample_table(int in, int out, std::vector<int32_t>& tab);
+bool ingest_rows_tables(const std::vector<int32_t>& tab_h, int ks_h, int W, int W2, int ks,
+                        std::vector<int32_t>& colmap, std::vector<int32_t>& sets);
+int ingest_rows_ks(int ks_h, int ks_v);
 void launch_ingest_rgb(const uint8_t* rgb, uint8_t* tmp, float* gray, const int32_t* tab_h, int ks_h,
-                       const int32_t* tab_v, int ks_v, int B, int H, int W, int H2, int W2, hipStream_t st);
+                       const int32_t* tab_v, int ks_v, const int32_t* colmap, const int32_t* sets, int nsets,
+                       int B, int H, int W, int H2, int W2, hipStream_t st);
 void launch_resize(const float* src, int sh, int sw, float* dst, int dh, int dw, int B,
                    hipStream_t st);
 

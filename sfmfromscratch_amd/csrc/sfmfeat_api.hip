@@ -57,6 +57,10 @@ struct sfm_ctx {
   // RGB temp of the horizontal pass; host staging for the host-pointer variant
   DevBuf i_tab_h, i_tab_v, i_tmp, i_rgb, i_gray;
   int i_w = -1, i_w2 = -1, i_h = -1, i_h2 = -1, i_ksh = 0, i_ksv = 0;
+  std::vector<int32_t> i_th, i_tv;  // host copies of the tables
+  DevBuf i_colmap, i_sets;          // row path (k_rows_h): column map + tap sets
+  int i_nsets = 0;
+  bool i_rows = false;
   bool match_direct = false;  // SFMFEAT_MATCH_DIRECT=1: all-pairs exact VALU kernel (A/B checks)
   bool exact_select = false;
   bool serial = false;        // SFMFEAT_SERIAL=1: no aux-stream overlap (diagnostic timings)  // SFMFEAT_SELECT=exact: every plane takes the exact-median path
@@ -507,7 +511,7 @@ int32_t sfm_ctx_destroy(sfm_ctx* c) {
                     &c->d_xy, &c->d_desc, &c->d_conf, &c->d_count, &c->d_u8, &c->m_desc, &c->m_count, &c->m_pairs,
                     &c->m_descT, &c->m_rows, &c->m_matches, &c->m_conf, &c->m_nmatch,
                     &c->m_hi, &c->m_lo, &c->m_norm2, &c->m_rnorm, &c->m_imgmax,
-                    &c->i_tab_h, &c->i_tab_v, &c->i_tmp, &c->i_rgb, &c->i_gray};
+                    &c->i_tab_h, &c->i_tab_v, &c->i_tmp, &c->i_rgb, &c->i_gray, &c->i_colmap, &c->i_sets};
   for (DevBuf* b : bufs) free_buf(*b);
   for (auto& e : c->prof_pending) {
     (void)hipEventDestroy(e.second.first);
@@ -562,25 +566,37 @@ namespace {
 int ingest_impl(sfm_ctx* c, const uint8_t* rgb, int B, int H, int W, int H2, int W2, float* gray,
                 hipStream_t st) {
   int rc;
-  if (c->i_w != W || c->i_w2 != W2) {
-    std::vector<int32_t> t;
-    c->i_ksh = build_resample_table(W, W2, t);
-    if ((rc = ensure(c, c->i_tab_h, t.size() * 4))) return rc;
-    HIPCHK(c, hipMemcpy(c->i_tab_h.p, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+  const bool newh = c->i_w != W || c->i_w2 != W2, newv = c->i_h != H || c->i_h2 != H2;
+  if (newh) {
+    c->i_ksh = build_resample_table(W, W2, c->i_th);
+    if ((rc = ensure(c, c->i_tab_h, c->i_th.size() * 4))) return rc;
+    HIPCHK(c, hipMemcpy(c->i_tab_h.p, c->i_th.data(), c->i_th.size() * 4, hipMemcpyHostToDevice));
     c->i_w = W;
     c->i_w2 = W2;
   }
-  if (c->i_h != H || c->i_h2 != H2) {
-    std::vector<int32_t> t;
-    c->i_ksv = build_resample_table(H, H2, t);
-    if ((rc = ensure(c, c->i_tab_v, t.size() * 4))) return rc;
-    HIPCHK(c, hipMemcpy(c->i_tab_v.p, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+  if (newv) {
+    c->i_ksv = build_resample_table(H, H2, c->i_tv);
+    if ((rc = ensure(c, c->i_tab_v, c->i_tv.size() * 4))) return rc;
+    HIPCHK(c, hipMemcpy(c->i_tab_v.p, c->i_tv.data(), c->i_tv.size() * 4, hipMemcpyHostToDevice));
     c->i_h = H;
     c->i_h2 = H2;
   }
-  if ((rc = ensure(c, c->i_tmp, (size_t)B * H * W2 * 3))) return rc;
+  if (newh || newv) {
+    std::vector<int32_t> cm, sets;
+    const int ks = ingest_rows_ks(c->i_ksh, c->i_ksv);
+    c->i_rows = ks && ingest_rows_tables(c->i_th, c->i_ksh, W, W2, ks, cm, sets);
+    if (c->i_rows) {
+      if ((rc = ensure(c, c->i_colmap, cm.size() * 4))) return rc;
+      if ((rc = ensure(c, c->i_sets, sets.size() * 4))) return rc;
+      HIPCHK(c, hipMemcpy(c->i_colmap.p, cm.data(), cm.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(c, hipMemcpy(c->i_sets.p, sets.data(), sets.size() * 4, hipMemcpyHostToDevice));
+      c->i_nsets = (int)(sets.size() / ks);
+    }
+  }
+  if ((rc = ensure(c, c->i_tmp, (size_t)B * H * W2 * 3 + 16))) return rc;
   launch_ingest_rgb(rgb, as<uint8_t>(c->i_tmp), gray, as<int32_t>(c->i_tab_h), c->i_ksh, as<int32_t>(c->i_tab_v),
-                    c->i_ksv, B, H, W, H2, W2, st);
+                    c->i_ksv, c->i_rows ? as<int32_t>(c->i_colmap) : nullptr, as<int32_t>(c->i_sets), c->i_nsets,
+                    B, H, W, H2, W2, st);
   HIPCHK(c, hipGetLastError());
   return SFM_OK;
 }
