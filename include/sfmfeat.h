@@ -143,6 +143,24 @@ int32_t sfm_ingest_rgb(sfm_ctx* ctx, const uint8_t* rgb, int32_t H, int32_t W, i
 /* (int(H * scale), int(W * scale)) — the PIL target size of Runner.py:37-42. */
 int32_t sfm_resize_dims(int32_t H, int32_t W, double scale, int32_t* H2, int32_t* W2);
 
+/*
+ * RANSAC inlier filter — replaces CameraPose.find_inliers (SFM.py:126-160), the match
+ * consumer of SFMRunner stage 1 (Runner.py:349-351).  p1, p2: n x 2 int64 pixel
+ * coordinates (the pairs of _convert_matches_to_coords, Runner.py:423-434); iters =
+ * max_iterations; samples replay numpy's legacy RandomState after np.random.seed(5).
+ * in1 / in2 (capacity n x 2) receive the winning sample's inliers in input order,
+ * n_out their count; n_out = -1 when n < 8 (the reference returns four Nones).
+ * best_iter (optional): the winning sample's index.
+ */
+int32_t sfm_ransac_find_inliers(sfm_ctx* ctx, const int64_t* p1, const int64_t* p2, int64_t n, int32_t iters,
+                                double threshold, int64_t* in1, int64_t* in2, int64_t* n_out,
+                                int32_t* best_iter);
+
+/* The sample indices np.random.choice(n, 8, replace=False) draws on each of `iters`
+ * iterations after np.random.seed(seed) (numpy legacy MT19937 + Fisher-Yates):
+ * out [iters][8] int32.  Host-only. */
+int32_t sfm_ransac_sample_indices(int32_t n, int32_t iters, uint32_t seed, int32_t* out);
+
 /* ---------------- device-resident batch API (throughput path) ----------------
  * All pointers are device pointers on the context's device; `stream` is the
  * hipStream_t the work is enqueued on, exactly as given (NULL = HIP's null stream, as
@@ -158,6 +176,15 @@ int32_t sfm_resize_dims(int32_t H, int32_t W, double scale, int32_t* H2, int32_t
  *   count [B] int32
  */
 int32_t sfm_reserve(sfm_ctx* ctx, int32_t B, int32_t H, int32_t W);
+
+/* sfm_ransac_find_inliers for P pairs at once: pts [P][nmax][4] int32 (x1, y1, x2, y2),
+ * npts [P] on the device and npts_host [P] on the host (the sample streams depend on n);
+ * out_pts [P][nmax][4] inliers in order, out_n [P] (-1 for n < 8), out_iter [P].
+ * nmax <= 2560.  Synchronises the stream before returning. */
+int32_t sfm_ransac_find_inliers_dev(sfm_ctx* ctx, const int32_t* pts, const int32_t* npts,
+                                    const int32_t* npts_host, int32_t P, int32_t nmax, int32_t iters,
+                                    double threshold, int32_t* out_pts, int32_t* out_n, int32_t* out_iter,
+                                    void* stream);
 
 /* sfm_ingest_rgb for B frames: rgb [B][H][W][3] uint8 -> gray [B][H2][W2] float32. */
 int32_t sfm_ingest_rgb_dev(sfm_ctx* ctx, const uint8_t* rgb, int32_t B, int32_t H, int32_t W,

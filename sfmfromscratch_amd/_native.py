@@ -44,6 +44,11 @@ SIGNATURES = {
     "sfm_ingest_rgb": (ctypes.c_int32, [_vp, _u8p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                         _fp]),
     "sfm_resize_dims": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_double, _i32p, _i32p]),
+    "sfm_ransac_find_inliers": (ctypes.c_int32, [_vp, _i64p, _i64p, ctypes.c_int64, ctypes.c_int32, ctypes.c_double,
+                                                 _i64p, _i64p, _i64p, _i32p]),
+    "sfm_ransac_sample_indices": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32, _i32p]),
+    "sfm_ransac_find_inliers_dev": (ctypes.c_int32, [_vp, _vp, _vp, _i32p, ctypes.c_int32, ctypes.c_int32,
+                                                     ctypes.c_int32, ctypes.c_double, _vp, _vp, _vp, _vp]),
     "sfm_ingest_rgb_dev": (ctypes.c_int32, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                             ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
     "sfm_extract_batch_dev": (ctypes.c_int32, [_vp, _vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _vp, _vp,
@@ -225,6 +230,23 @@ class Context:
         check(self.lib.sfm_ingest_rgb(self.handle, rgb.ctypes.data_as(_u8p), H, W, H2, W2, out.ctypes.data_as(_fp)),
               self.handle)
         return out
+
+    def ransac_find_inliers(self, p1: np.ndarray, p2: np.ndarray, threshold: float, iters: int):
+        """-> (in1 (k,2) int64, in2 (k,2) int64, best_iter) or None when n < 8."""
+        p1 = np.ascontiguousarray(p1, np.int64).reshape(-1, 2)
+        p2 = np.ascontiguousarray(p2, np.int64).reshape(-1, 2)
+        n = p1.shape[0]
+        o1 = np.empty((max(n, 1), 2), np.int64)
+        o2 = np.empty((max(n, 1), 2), np.int64)
+        k = ctypes.c_int64(0)
+        bi = ctypes.c_int32(-1)
+        check(self.lib.sfm_ransac_find_inliers(self.handle, p1.ctypes.data_as(_i64p), p2.ctypes.data_as(_i64p), n,
+                                               int(iters), ctypes.c_double(threshold), o1.ctypes.data_as(_i64p),
+                                               o2.ctypes.data_as(_i64p), ctypes.byref(k), ctypes.byref(bi)),
+              self.handle)
+        if k.value < 0:
+            return None
+        return o1[:k.value], o2[:k.value], int(bi.value)
 
     # -------- device-pointer API (throughput path; pointers are ints) --------
     def ingest_rgb_dev(self, rgb_ptr: int, B: int, H: int, W: int, H2: int, W2: int, gray_ptr: int,

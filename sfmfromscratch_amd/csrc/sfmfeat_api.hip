@@ -58,6 +58,9 @@ struct sfm_ctx {
   DevBuf i_tab_h, i_tab_v, i_tmp, i_rgb, i_gray;
   int i_w = -1, i_w2 = -1, i_h = -1, i_h2 = -1, i_ksh = 0, i_ksv = 0;
   std::vector<int32_t> i_th, i_tv;  // host copies of the tables
+  // RANSAC (sfm_ransac_*): sample-index streams cached per (n, iterations), device buffers
+  std::vector<std::pair<std::pair<int, int>, std::vector<int32_t>>> r_cache;
+  DevBuf r_idx, r_off, r_F, r_counts, r_pts, r_npts, r_out, r_on, r_oit;
   DevBuf i_colmap, i_sets;          // row path (k_rows_h): column map + tap sets
   int i_nsets = 0;
   bool i_rows = false;
@@ -511,7 +514,9 @@ int32_t sfm_ctx_destroy(sfm_ctx* c) {
                     &c->d_xy, &c->d_desc, &c->d_conf, &c->d_count, &c->d_u8, &c->m_desc, &c->m_count, &c->m_pairs,
                     &c->m_descT, &c->m_rows, &c->m_matches, &c->m_conf, &c->m_nmatch,
                     &c->m_hi, &c->m_lo, &c->m_norm2, &c->m_rnorm, &c->m_imgmax,
-                    &c->i_tab_h, &c->i_tab_v, &c->i_tmp, &c->i_rgb, &c->i_gray, &c->i_colmap, &c->i_sets};
+                    &c->i_tab_h, &c->i_tab_v, &c->i_tmp, &c->i_rgb, &c->i_gray, &c->i_colmap, &c->i_sets,
+                    &c->r_idx, &c->r_off, &c->r_F, &c->r_counts, &c->r_pts, &c->r_npts, &c->r_out, &c->r_on,
+                    &c->r_oit};
   for (DevBuf* b : bufs) free_buf(*b);
   for (auto& e : c->prof_pending) {
     (void)hipEventDestroy(e.second.first);
@@ -623,6 +628,119 @@ int32_t sfm_ingest_rgb(sfm_ctx* c, const uint8_t* rgb, int32_t H, int32_t W, int
   if ((rc = ingest_impl(c, as<uint8_t>(c->i_rgb), 1, H, W, H2, W2, as<float>(c->i_gray), st))) return rc;
   HIPCHK(c, hipMemcpyAsync(gray, c->i_gray.p, (size_t)H2 * W2 * 4, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
+  return SFM_OK;
+}
+
+int32_t sfm_ransac_sample_indices(int32_t n, int32_t iters, uint32_t seed, int32_t* out) {
+  if (n < 8 || iters < 0 || !out) return SFM_EINVAL;
+  ransac_sample_indices(n, iters, seed, out);
+  return SFM_OK;
+}
+
+namespace {
+const std::vector<int32_t>& ransac_stream(sfm_ctx* c, int n, int iters) {
+  for (auto& e : c->r_cache)
+    if (e.first.first == n && e.first.second == iters) return e.second;
+  if (c->r_cache.size() >= 64) c->r_cache.erase(c->r_cache.begin());
+  c->r_cache.push_back({{n, iters}, std::vector<int32_t>((size_t)iters * 8)});
+  ransac_sample_indices(n, iters, 5u, c->r_cache.back().second.data());  // np.random.seed(5), SFM.py:133
+  return c->r_cache.back().second;
+}
+
+int ransac_impl(sfm_ctx* c, const int32_t* pts, const int32_t* npts_dev, const int32_t* npts_host, int P, int nmax,
+                int iters, double thr, int32_t* out_pts, int32_t* out_n, int32_t* out_iter, hipStream_t st) {
+  if (nmax > ransac_max_points()) return set_err(c, SFM_EINVAL, "more than 2560 correspondences per pair");
+  // sample streams (host replay of numpy's RandomState; identical for equal n)
+  std::vector<int32_t> all, off(P, 0);
+  std::vector<int> seen_n;
+  std::vector<int32_t> seen_off;
+  for (int p = 0; p < P; ++p) {
+    const int n = npts_host[p];
+    if (n < 8 || n > nmax) {
+      if (n > nmax) return set_err(c, SFM_EINVAL, "correspondence count above nmax");
+      continue;
+    }
+    int k = -1;
+    for (size_t i = 0; i < seen_n.size(); ++i)
+      if (seen_n[i] == n) k = (int)i;
+    if (k < 0) {
+      const std::vector<int32_t>& s = ransac_stream(c, n, iters);
+      seen_n.push_back(n);
+      seen_off.push_back((int32_t)all.size());
+      all.insert(all.end(), s.begin(), s.end());
+      k = (int)seen_n.size() - 1;
+    }
+    off[p] = seen_off[k];
+  }
+  if (all.empty()) all.assign(8, 0);
+  int rc;
+  if ((rc = ensure(c, c->r_idx, all.size() * 4))) return rc;
+  if ((rc = ensure(c, c->r_off, (size_t)P * 4))) return rc;
+  if ((rc = ensure(c, c->r_F, (size_t)P * std::max(iters, 1) * 9 * 8))) return rc;
+  if ((rc = ensure(c, c->r_counts, (size_t)P * std::max(iters, 1) * 4))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->r_idx.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->r_off.p, off.data(), (size_t)P * 4, hipMemcpyHostToDevice, st));
+  if (iters > 0)
+    launch_ransac(pts, npts_dev, nmax, P, as<int32_t>(c->r_idx), as<int32_t>(c->r_off), iters, thr, as<double>(c->r_F),
+                  as<int32_t>(c->r_counts), out_pts, out_n, out_iter, st);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(st));  // the host index buffers above are stack-owned
+  return SFM_OK;
+}
+}  // namespace
+
+int32_t sfm_ransac_find_inliers_dev(sfm_ctx* c, const int32_t* pts, const int32_t* npts, const int32_t* npts_host,
+                                    int32_t P, int32_t nmax, int32_t iters, double threshold, int32_t* out_pts,
+                                    int32_t* out_n, int32_t* out_iter, void* stream) {
+  if (!c || !pts || !npts || !npts_host || !out_pts || !out_n || !out_iter || P < 1 || nmax < 1 || iters < 0)
+    return SFM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  return ransac_impl(c, pts, npts, npts_host, P, nmax, iters, threshold, out_pts, out_n, out_iter,
+                     (hipStream_t)stream);
+}
+
+int32_t sfm_ransac_find_inliers(sfm_ctx* c, const int64_t* p1, const int64_t* p2, int64_t n, int32_t iters,
+                                double threshold, int64_t* in1, int64_t* in2, int64_t* n_out, int32_t* best_iter) {
+  if (!c || !n_out || n < 0 || iters < 0 || (n > 0 && (!p1 || !p2))) return SFM_EINVAL;
+  if (n > ransac_max_points()) return set_err(c, SFM_EINVAL, "more than 2560 correspondences");
+  HIPCHK(c, hipSetDevice(c->device));
+  *n_out = -1;
+  if (n < 8) return SFM_OK;  // the reference returns (None, None, None, None)
+  const int nmax = (int)n;
+  std::vector<int32_t> h((size_t)nmax * 4);
+  for (int64_t i = 0; i < n; ++i) {
+    h[4 * i + 0] = (int32_t)p1[2 * i];
+    h[4 * i + 1] = (int32_t)p1[2 * i + 1];
+    h[4 * i + 2] = (int32_t)p2[2 * i];
+    h[4 * i + 3] = (int32_t)p2[2 * i + 1];
+  }
+  int rc;
+  if ((rc = ensure(c, c->r_pts, h.size() * 4))) return rc;
+  if ((rc = ensure(c, c->r_npts, 16))) return rc;
+  if ((rc = ensure(c, c->r_out, h.size() * 4))) return rc;
+  if ((rc = ensure(c, c->r_on, 16))) return rc;
+  if ((rc = ensure(c, c->r_oit, 16))) return rc;
+  hipStream_t st = c->stream;
+  const int32_t nn = (int32_t)n;
+  HIPCHK(c, hipMemcpyAsync(c->r_pts.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, st));
+  HIPCHK(c, hipMemcpyAsync(c->r_npts.p, &nn, 4, hipMemcpyHostToDevice, st));
+  if ((rc = ransac_impl(c, as<int32_t>(c->r_pts), as<int32_t>(c->r_npts), &nn, 1, nmax, iters, threshold,
+                        as<int32_t>(c->r_out), as<int32_t>(c->r_on), as<int32_t>(c->r_oit), st)))
+    return rc;
+  int32_t k = 0, bi = -1;
+  HIPCHK(c, hipMemcpyAsync(&k, c->r_on.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipMemcpyAsync(&bi, c->r_oit.p, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
+  if (k > 0) {
+    std::vector<int32_t> o((size_t)k * 4);
+    HIPCHK(c, hipMemcpy(o.data(), c->r_out.p, o.size() * 4, hipMemcpyDeviceToHost));
+    for (int i = 0; i < k; ++i) {
+      if (in1) { in1[2 * i] = o[4 * i]; in1[2 * i + 1] = o[4 * i + 1]; }
+      if (in2) { in2[2 * i] = o[4 * i + 2]; in2[2 * i + 1] = o[4 * i + 3]; }
+    }
+  }
+  *n_out = k;
+  if (best_iter) *best_iter = bi;
   return SFM_OK;
 }
 

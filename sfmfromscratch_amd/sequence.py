@@ -209,20 +209,38 @@ def match_schedule(cache: FeatureCache, pairs: np.ndarray, ratio_threshold: floa
 
 
 def stage1(img_path: str, max_img: int, extractor_params: dict, match_threshold: float = 0.85,
-           single_K=None, scale_factor: float = 0.5, num_matches: int = 2500, device: int = 0):
+           single_K=None, scale_factor: float = 0.5, num_matches: int = 2500, device: int = 0,
+           ransac: bool = False, ransac_max_it: int | None = None):
     """SFMRunner.perform's stage 1 (Runner.py:183-191): frames "{img_path}/{i}.jpg" for
     i = 1..max_img, consecutive pairs; returns all_matches[(max_img+1) x (max_img+1)] of
-    Matches as the reference fills it (Runner.py:174-175, 354-355)."""
+    Matches as the reference fills it (Runner.py:174-175, 354-355).  With ransac=True the
+    pairs other than (1, 2) get the reference's inlier filter (Runner.py:349-351,
+    pose.find_inliers with max_iterations = ransac_max_it, default
+    calculate_num_ransac_iterations(0.98, 8, 0.4) as Runner.py:170), all pairs in one
+    device pass; a pair with fewer than 8 correspondences raises ValueError, as the
+    reference's tuple unpacking of find_inliers' four Nones does."""
     paths = ["{}/{}.jpg".format(img_path, i) for i in range(1, max_img + 1)]
     cache = FeatureCache(paths, extractor_params, scale_factor=scale_factor, device=device)
     pairs = pair_schedule(max_img, "consecutive")
     res = match_schedule(cache, pairs, match_threshold)
     all_matches = [[None for _ in range(max_img + 1)] for _ in range(max_img + 1)]
+    coords = []
     for (a, b), (mm, cc) in zip(pairs, res):
-        i1, i2 = int(a) + 1, int(b) + 1
         X1, Y1 = cache.keypoints(int(a))
         X2, Y2 = cache.keypoints(int(b))
-        p1, p2 = convert_matches_to_coords(mm, X1, Y1, X2, Y2, num_matches)
+        coords.append(convert_matches_to_coords(mm, X1, Y1, X2, Y2, num_matches))
+    if ransac:
+        from . import pose
+        iters = ransac_max_it if ransac_max_it is not None else pose.calculate_num_ransac_iterations(0.98, 8, 0.4)
+        sel = [k for k, (a, b) in enumerate(pairs) if (int(a) + 1, int(b) + 1) != (1, 2)]
+        filt = pose.find_inliers_batch([coords[k] for k in sel], max_iterations=iters, device=device)
+        for k, r in zip(sel, filt):
+            if len(r) != 2:
+                raise ValueError("too many values to unpack (expected 2)")  # Runner.py:351 on four Nones
+            coords[k] = r
+    for k, ((a, b), (mm, cc)) in enumerate(zip(pairs, res)):
+        i1, i2 = int(a) + 1, int(b) + 1
+        p1, p2 = coords[k]
         all_matches[i1][i2] = Matches(mm, cc, p1, p2, single_K, single_K)
         all_matches[i2][i1] = Matches(mm, cc, p2, p1, single_K, single_K)
     return all_matches, cache

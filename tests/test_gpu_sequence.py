@@ -62,3 +62,22 @@ def test_cache_all_pairs_and_mixed_sizes_vs_dropin(tmp_path):
     cache.save(p)
     X2, Y2, D2 = S.load_features(p)
     assert np.array_equal(D2[4], cache.descriptors(4))
+
+
+def test_stage1_with_ransac_vs_oracle(tmp_path):
+    """Runner.py:349-351: every pair but (1, 2) filtered by find_inliers (reference
+    iteration count), batched on the device == the oracle's find_inliers per pair."""
+    Image = pytest.importorskip("PIL.Image")
+    from oracle import ransac as R
+    from sfmfromscratch_amd import sequence as S
+    n = 4
+    for i in range(n):
+        Image.fromarray(synth.make_frame_rgb_u8(360, 640, 51, i)).save(str(tmp_path / f"{i + 1}.jpg"), quality=95)
+    pp = dict(P_OCT, num_interest_points=600)
+    raw, _ = S.stage1(str(tmp_path), n, pp)
+    filt, _ = S.stage1(str(tmp_path), n, pp, ransac=True, ransac_max_it=400)
+    assert np.array_equal(filt[1][2].p1, raw[1][2].p1)  # the initial pair is not filtered
+    for i1 in (2, 3):
+        o = R.find_inliers(raw[i1][i1 + 1].p1, raw[i1][i1 + 1].p2, 1.0, 400)
+        assert np.array_equal(filt[i1][i1 + 1].p1, o[0]) and np.array_equal(filt[i1][i1 + 1].p2, o[1])
+        assert np.array_equal(filt[i1 + 1][i1].p1, o[1])

@@ -231,6 +231,53 @@ def gen_ingest():
     save("ingest.npz", **out)
 
 
+def ransac_cases():
+    """Correspondence sets for the RANSAC consumer (SFM.py:126-160): matched keypoints of
+    synthetic frame pairs through the oracle's extract + match and the reference's own
+    _convert_matches_to_coords rule (first 2,500 matches, Runner.py:423-434), a planted
+    translation with outliers, and a set below 8 points."""
+    from oracle import oracle as O
+    cases = []
+    for (H, W, seed, iters, thr) in [(540, 960, 77, 5967, 1.0), (720, 1280, 78, 1500, 1.0), (540, 960, 79, 800, 0.5)]:
+        f = [synth.make_frame(H, W, seed, i) for i in range(2)]
+        E = [O.extract(x, P_OCT) for x in f]
+        m, _ = O.match(E[0][2], E[1][2], 0.85)
+        mm = m[:2500]
+        p1 = np.column_stack((E[0][0][mm[:, 0]], E[0][1][mm[:, 0]]))
+        p2 = np.column_stack((E[1][0][mm[:, 1]], E[1][1][mm[:, 1]]))
+        cases.append((p1, p2, iters, thr))
+    rng = np.random.default_rng(5)
+    p1 = rng.integers(0, 900, (300, 2)).astype(np.int64)
+    p2 = p1 + np.array([3, 2])
+    out = rng.random(300) < 0.3
+    p2[out] = rng.integers(0, 900, (int(out.sum()), 2))
+    cases.append((p1, p2, 500, 1.0))
+    cases.append((p1[:7], p2[:7], 100, 1.0))
+    return cases
+
+
+def gen_ransac():
+    """The reference's CameraPose.find_inliers itself on ransac_cases() (its cv2 import is
+    the stand-in; find_inliers uses numpy only)."""
+    from SFM import CameraPose
+    out = {}
+    cases = ransac_cases()
+    out["ncases"] = np.int64(len(cases))
+    for i, (p1, p2, iters, thr) in enumerate(cases):
+        t0 = time.time()
+        r = CameraPose.find_inliers(p1, p2, threshold=thr, max_iterations=iters)
+        out[f"c{i}_p1"], out[f"c{i}_p2"] = p1, p2
+        out[f"c{i}_meta"] = np.array([iters], np.int64)
+        out[f"c{i}_thr"] = np.float64(thr)
+        if len(r) == 4:  # fewer than 8 points: (None, None, None, None)
+            out[f"c{i}_none"] = np.int64(1)
+        else:
+            out[f"c{i}_in1"], out[f"c{i}_in2"] = np.asarray(r[0]), np.asarray(r[1])
+        print(f"  case {i}: n={len(p1)} iters={iters} -> {'None' if len(r) == 4 else len(r[0])} "
+              f"({time.time() - t0:.1f} s)")
+    save("ransac.npz", **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-1080p", action="store_true")
@@ -245,6 +292,7 @@ def main():
         "descriptors": gen_descriptors,
         "match": gen_match,
         "ingest": gen_ingest,
+        "ransac": gen_ransac,
         "small": lambda: (gen_extract("extract_small_scalerot.npz", 150, 200, 21, P_OCT, "scalerot"),
                           gen_extract("extract_small_pmain.npz", 151, 203, 22, P_MAIN, "scalerot"),
                           gen_extract("extract_small_naive.npz", 150, 200, 23, {"num_interest_points": 500},
