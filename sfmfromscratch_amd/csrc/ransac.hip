@@ -28,6 +28,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "kernels.h"
@@ -60,20 +62,72 @@ struct MT19937 {
     return y;
   }
 };
+
+// The tempered output stream of one seed, generated once per process in fixed chunks
+// that never move: every pair restarts from np.random.seed(5) (SFM.py:133), so all
+// pairs read the same raw words and differ only in how their n consumes them.
+class RawStream {
+ public:
+  static constexpr size_t kChunk = size_t(1) << 20;
+  explicit RawStream(uint32_t seed) : g_(seed) {}
+  const uint32_t* chunk(size_t k) {
+    std::lock_guard<std::mutex> lock(mu_);
+    while (chunks_.size() <= k) {
+      std::unique_ptr<uint32_t[]> c(new uint32_t[kChunk]);
+      for (size_t i = 0; i < kChunk; ++i) c[i] = g_.next();
+      chunks_.push_back(std::move(c));
+    }
+    return chunks_[k].get();
+  }
+
+ private:
+  std::mutex mu_;
+  MT19937 g_;
+  std::vector<std::unique_ptr<uint32_t[]>> chunks_;
+};
+
+RawStream& raw_stream(uint32_t seed) {
+  static std::mutex mu;
+  static std::vector<std::pair<uint32_t, std::unique_ptr<RawStream>>> streams;
+  std::lock_guard<std::mutex> lock(mu);
+  for (auto& s : streams)
+    if (s.first == seed) return *s.second;
+  streams.emplace_back(seed, std::unique_ptr<RawStream>(new RawStream(seed)));
+  return *streams.back().second;
+}
+
+struct Cursor {
+  RawStream& s;
+  size_t k = 0, i = 0;
+  const uint32_t* c;
+  explicit Cursor(RawStream& st) : s(st), c(st.chunk(0)) {}
+  uint32_t next() {
+    if (i == RawStream::kChunk) {
+      c = s.chunk(++k);
+      i = 0;
+    }
+    return c[i++];
+  }
+};
 }  // namespace
 
 void ransac_sample_indices(int n, int iters, uint32_t seed, int32_t* out) {
-  MT19937 g(seed);
-  std::vector<int32_t> a(n);
+  Cursor g(raw_stream(seed));
+  std::vector<int32_t> a(std::max(n, 1));
+  uint32_t top = 0;  // random_interval's mask for i = n - 1: the smallest 2^b - 1 >= i
+  if (n > 1) {
+    top = (uint32_t)(n - 1);
+    top |= top >> 1;
+    top |= top >> 2;
+    top |= top >> 4;
+    top |= top >> 8;
+    top |= top >> 16;
+  }
   for (int it = 0; it < iters; ++it) {
     for (int i = 0; i < n; ++i) a[i] = i;
+    uint32_t mask = top;
     for (int i = n - 1; i >= 1; --i) {  // _shuffle_raw: j = random_interval(i)
-      uint32_t mask = (uint32_t)i;
-      mask |= mask >> 1;
-      mask |= mask >> 2;
-      mask |= mask >> 4;
-      mask |= mask >> 8;
-      mask |= mask >> 16;
+      if ((uint32_t)i <= (mask >> 1)) mask >>= 1;  // i drops by one: one halving keeps it minimal
       uint32_t v;
       while ((v = (g.next() & mask)) > (uint32_t)i) {
       }
@@ -152,6 +206,42 @@ SFM_DEV bool null_vector_8x9(double (&A)[8][9], double (&f)[9]) {
   return true;
 }
 
+// The same elimination when every column 0..7 has a pivot (the usual case), with every
+// index compile-time: row exchanges are selects, so A stays in registers (the general
+// routine's runtime row indices put it in scratch).  Returns false on a zero pivot; the
+// caller then rebuilds A and takes the general routine, which handles free columns.
+SFM_DEV bool null_vector_8x9_regs(double (&A)[8][9], double (&f)[9]) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+#pragma unroll
+    for (int i = c + 1; i < 8; ++i) {  // the first row of largest |A[.][c]| ends in row c
+      const bool sw = fabs(A[i][c]) > fabs(A[c][c]);
+#pragma unroll
+      for (int k = c; k < 9; ++k) {
+        const double u = A[c][k], v = A[i][k];
+        A[c][k] = sw ? v : u;
+        A[i][k] = sw ? u : v;
+      }
+    }
+    if (!(fabs(A[c][c]) >= 1e-300)) return false;
+#pragma unroll
+    for (int i = c + 1; i < 8; ++i) {
+      const double fct = A[i][c] / A[c][c];
+#pragma unroll
+      for (int k = c; k < 9; ++k) A[i][k] -= fct * A[c][k];
+    }
+  }
+  f[8] = 1.0;
+#pragma unroll
+  for (int i = 7; i >= 0; --i) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = i + 1; k < 9; ++k) acc += A[i][k] * f[k];
+    f[i] = -acc / A[i][i];
+  }
+  return true;
+}
+
 // smallest-eigenvalue eigenvector of a symmetric 3 x 3 (cyclic Jacobi)
 SFM_DEV void smallest_eigvec3(double (&S)[3][3], double (&v)[3]) {
   double V[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
@@ -159,7 +249,9 @@ SFM_DEV void smallest_eigvec3(double (&S)[3][3], double (&v)[3]) {
     const double off = fabs(S[0][1]) + fabs(S[0][2]) + fabs(S[1][2]);
     const double dia = fabs(S[0][0]) + fabs(S[1][1]) + fabs(S[2][2]);
     if (off <= 1e-18 * dia) break;
+#pragma unroll
     for (int p = 0; p < 2; ++p)
+#pragma unroll
       for (int q = p + 1; q < 3; ++q) {
         if (fabs(S[p][q]) < 1e-300) continue;
         const double theta = (S[q][q] - S[p][p]) / (2.0 * S[p][q]);
@@ -182,10 +274,9 @@ SFM_DEV void smallest_eigvec3(double (&S)[3][3], double (&v)[3]) {
         }
       }
   }
-  int mi = 0;
-  for (int i = 1; i < 3; ++i)
-    if (S[i][i] < S[mi][mi]) mi = i;
-  for (int k = 0; k < 3; ++k) v[k] = V[k][mi];
+  const int mi = (S[1][1] < S[0][0]) ? ((S[2][2] < S[1][1]) ? 2 : 1) : ((S[2][2] < S[0][0]) ? 2 : 0);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) v[k] = mi == 0 ? V[k][0] : (mi == 1 ? V[k][1] : V[k][2]);  // no runtime index
 }
 
 // one thread per (pair, sample): F as 9 doubles (NaN for degenerate samples)
@@ -214,15 +305,23 @@ __global__ void __launch_bounds__(128) k_ransac_F(const int32_t* __restrict__ pt
   normalise8(x1, y1, a1, b1, s1, c1x, c1y);
   normalise8(x2, y2, a2, b2, s2, c2x, c2y);
   double A[8][9];
+  auto build = [&]() {
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const double u1 = a1[i], v1 = b1[i], u2 = a2[i], v2 = b2[i];
-    A[i][0] = u1 * u2; A[i][1] = v1 * u2; A[i][2] = u2;
-    A[i][3] = u1 * v2; A[i][4] = v1 * v2; A[i][5] = v2;
-    A[i][6] = u1;      A[i][7] = v1;      A[i][8] = 1.0;
-  }
+    for (int i = 0; i < 8; ++i) {
+      const double u1 = a1[i], v1 = b1[i], u2 = a2[i], v2 = b2[i];
+      A[i][0] = u1 * u2; A[i][1] = v1 * u2; A[i][2] = u2;
+      A[i][3] = u1 * v2; A[i][4] = v1 * v2; A[i][5] = v2;
+      A[i][6] = u1;      A[i][7] = v1;      A[i][8] = 1.0;
+    }
+  };
+  build();
   double f[9];
-  if (!null_vector_8x9(A, f)) {
+  bool ok = null_vector_8x9_regs(A, f);
+  if (!ok) {  // a zero pivot: the general elimination (free-column search) on a fresh system
+    build();
+    ok = null_vector_8x9(A, f);
+  }
+  if (!ok) {
 #pragma unroll
     for (int k = 0; k < 9; ++k) F[k] = NAN;
     return;
@@ -254,13 +353,21 @@ __global__ void __launch_bounds__(128) k_ransac_F(const int32_t* __restrict__ pt
     for (int c = 0; c < 3; ++c) F[3 * r + c] = T2[0][r] * M[0][c] + T2[1][r] * M[1][c] + T2[2][r] * M[2][c];
 }
 
+// d = |l . p2| / sqrt(l0^2 + l1^2) < thr (SFM.py:148-153).  Decided as num^2 vs thr^2 den2
+// unless the two are within a relative 2^-40 of each other, where the reference's own
+// expression decides: the squared comparison cannot flip a point farther than that from
+// the threshold, and spares the float64 division and square root almost everywhere.
 SFM_DEV bool epi_inlier(const double* F, double x1, double y1, double x2, double y2, double thr) {
   const double l0 = F[0] * x1 + F[1] * y1 + F[2];
   const double l1 = F[3] * x1 + F[4] * y1 + F[5];
   const double l2 = F[6] * x1 + F[7] * y1 + F[8];
   const double num = fabs((l0 * x2 + l1 * y2) + l2);
-  const double d = num / sqrt(l0 * l0 + l1 * l1);
-  return d < thr;  // NaN (degenerate F) -> false
+  const double den2 = l0 * l0 + l1 * l1;
+  if (!(thr > 0.0)) return false;  // d >= 0 (or NaN) is never below a threshold <= 0
+  const double a = num * num, b = (thr * thr) * den2;
+  if (a < b * (1.0 - 0x1p-40)) return true;
+  if (a > b * (1.0 + 0x1p-40)) return false;
+  return num / sqrt(den2) < thr;  // near the threshold, or NaN (degenerate F) -> false
 }
 
 // inlier count per (pair, sample): one wave per sample, points in LDS

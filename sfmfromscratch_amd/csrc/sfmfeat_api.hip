@@ -14,7 +14,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sfmfeat.h"
@@ -638,19 +640,58 @@ int32_t sfm_ransac_sample_indices(int32_t n, int32_t iters, uint32_t seed, int32
 }
 
 namespace {
-const std::vector<int32_t>& ransac_stream(sfm_ctx* c, int n, int iters) {
+constexpr size_t kRansacCacheCap = 256;  // cached (n, iterations) streams per context (~190 KB each)
+
+const std::vector<int32_t>* ransac_cached(sfm_ctx* c, int n, int iters) {
   for (auto& e : c->r_cache)
-    if (e.first.first == n && e.first.second == iters) return e.second;
-  if (c->r_cache.size() >= 64) c->r_cache.erase(c->r_cache.begin());
-  c->r_cache.push_back({{n, iters}, std::vector<int32_t>((size_t)iters * 8)});
-  ransac_sample_indices(n, iters, 5u, c->r_cache.back().second.data());  // np.random.seed(5), SFM.py:133
-  return c->r_cache.back().second;
+    if (e.first.first == n && e.first.second == iters) return &e.second;
+  return nullptr;
+}
+
+// Replays the sample streams of every size in `ns` not cached yet, the sizes spread over
+// host threads (each walks the shared raw MT19937 words on its own), and caches them.
+void ransac_prefetch_streams(sfm_ctx* c, const std::vector<int>& ns, int iters) {
+  std::vector<int> todo;
+  for (int n : ns)
+    if (!ransac_cached(c, n, iters)) todo.push_back(n);
+  if (todo.empty()) return;
+  std::vector<std::vector<int32_t>> out(todo.size());
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (size_t i; (i = next.fetch_add(1)) < todo.size();) {
+      out[i].resize((size_t)iters * 8);
+      ransac_sample_indices(todo[i], iters, 5u, out[i].data());  // np.random.seed(5), SFM.py:133
+    }
+  };
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const size_t nt = std::min<size_t>(todo.size(), hw);
+  std::vector<std::thread> pool;
+  for (size_t t = 1; t < nt; ++t) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+  for (size_t i = 0; i < todo.size(); ++i) c->r_cache.push_back({{todo[i], iters}, std::move(out[i])});
+  // trim: the oldest streams this call does not use go first
+  for (auto it = c->r_cache.begin(); c->r_cache.size() > kRansacCacheCap && it != c->r_cache.end();) {
+    if (it->first.second != iters || std::find(ns.begin(), ns.end(), it->first.first) == ns.end())
+      it = c->r_cache.erase(it);
+    else
+      ++it;
+  }
 }
 
 int ransac_impl(sfm_ctx* c, const int32_t* pts, const int32_t* npts_dev, const int32_t* npts_host, int P, int nmax,
                 int iters, double thr, int32_t* out_pts, int32_t* out_n, int32_t* out_iter, hipStream_t st) {
   if (nmax > ransac_max_points()) return set_err(c, SFM_EINVAL, "more than 2560 correspondences per pair");
   // sample streams (host replay of numpy's RandomState; identical for equal n)
+  {
+    std::vector<int> ns;
+    for (int p = 0; p < P; ++p) {
+      const int n = npts_host[p];
+      if (n > nmax) return set_err(c, SFM_EINVAL, "correspondence count above nmax");
+      if (n >= 8 && std::find(ns.begin(), ns.end(), n) == ns.end()) ns.push_back(n);
+    }
+    ransac_prefetch_streams(c, ns, iters);
+  }
   std::vector<int32_t> all, off(P, 0);
   std::vector<int> seen_n;
   std::vector<int32_t> seen_off;
@@ -664,7 +705,7 @@ int ransac_impl(sfm_ctx* c, const int32_t* pts, const int32_t* npts_dev, const i
     for (size_t i = 0; i < seen_n.size(); ++i)
       if (seen_n[i] == n) k = (int)i;
     if (k < 0) {
-      const std::vector<int32_t>& s = ransac_stream(c, n, iters);
+      const std::vector<int32_t>& s = *ransac_cached(c, n, iters);
       seen_n.push_back(n);
       seen_off.push_back((int32_t)all.size());
       all.insert(all.end(), s.begin(), s.end());
