@@ -17,8 +17,9 @@
 //   removing the smallest singular direction (F - (F v3) v3^T, v3 from a Jacobi
 //   eigen-decomposition of F^T F: equal to U diag(d1, d2, 0) V^T), un-normalised.
 //   Distances are invariant to F's scale and sign.
-// * Inlier counts (SFM.py:147-156): one wave per sample at a time, points staged in LDS,
-//   d = |lb . p2| / sqrt(lb0^2 + lb1^2) with lb = F p1 in float64, d < threshold.
+// * Inlier counts (SFM.py:147-156): one thread per sample, the pair's points staged in LDS
+//   and read as broadcasts, d = |lb . p2| / sqrt(lb0^2 + lb1^2) with lb = F p1 in
+//   float64, d < threshold (decided without the division away from the threshold).
 // * Selection: the first sample with the largest count (strict > updates, SFM.py:156),
 //   its mask recomputed and the inliers compacted in input order.
 // Bar: the inlier sets equal the reference's on the golden pairs; float64 rounding of
@@ -357,48 +358,63 @@ __global__ void __launch_bounds__(128) k_ransac_F(const int32_t* __restrict__ pt
 // unless the two are within a relative 2^-40 of each other, where the reference's own
 // expression decides: the squared comparison cannot flip a point farther than that from
 // the threshold, and spares the float64 division and square root almost everywhere.
-SFM_DEV bool epi_inlier(const double* F, double x1, double y1, double x2, double y2, double thr) {
-  const double l0 = F[0] * x1 + F[1] * y1 + F[2];
-  const double l1 = F[3] * x1 + F[4] * y1 + F[5];
-  const double l2 = F[6] * x1 + F[7] * y1 + F[8];
-  const double num = fabs((l0 * x2 + l1 * y2) + l2);
-  const double den2 = l0 * l0 + l1 * l1;
-  if (!(thr > 0.0)) return false;  // d >= 0 (or NaN) is never below a threshold <= 0
-  const double a = num * num, b = (thr * thr) * den2;
-  if (a < b * (1.0 - 0x1p-40)) return true;
-  if (a > b * (1.0 + 0x1p-40)) return false;
+// lb = F p1 as fmas (numpy's F @ a_h goes through BLAS, whose order and fusing are its
+// own; the bar is set by F's float64 rounding anyway).  thr2lo / thr2hi = thr^2 (1 -+ 2^-40).
+SFM_DEV bool epi_inlier(const double* F, double x1, double y1, double x2, double y2, double thr, double thr2lo,
+                        double thr2hi) {
+  const double l0 = __builtin_fma(F[0], x1, __builtin_fma(F[1], y1, F[2]));
+  const double l1 = __builtin_fma(F[3], x1, __builtin_fma(F[4], y1, F[5]));
+  const double l2 = __builtin_fma(F[6], x1, __builtin_fma(F[7], y1, F[8]));
+  const double num = fabs(__builtin_fma(l0, x2, __builtin_fma(l1, y2, l2)));
+  const double den2 = __builtin_fma(l0, l0, l1 * l1);
+  const double a = num * num;
+  if (a < thr2lo * den2) return true;
+  if (a > thr2hi * den2) return false;
   return num / sqrt(den2) < thr;  // near the threshold, or NaN (degenerate F) -> false
 }
 
-// inlier count per (pair, sample): one wave per sample, points in LDS
+struct EpiThr {
+  double thr, lo, hi;
+};
+SFM_DEV EpiThr epi_thr(double thr) {  // thr <= 0 (or NaN): nothing is an inlier (d >= 0)
+  const double t2 = thr * thr;
+  const bool on = thr > 0.0;
+  return {thr, on ? t2 * (1.0 - 0x1p-40) : -1.0, on ? t2 * (1.0 + 0x1p-40) : -1.0};
+}
+
+// inlier count per (pair, sample): one thread per sample, its F in registers for the whole
+// sweep; the pair's points are staged in LDS as float64 (x1, y1, x2, y2) and every lane
+// reads the same point (a broadcast) — no per-sample reduction, F reload or conversion
 constexpr int kRansacMaxPts = 2560;
 __global__ void __launch_bounds__(256) k_ransac_count(const int32_t* __restrict__ pts,
                                                       const int32_t* __restrict__ npts, int nmax,
                                                       const double* __restrict__ Fs, int iters, double thr,
                                                       int32_t* __restrict__ counts) {
-  __shared__ int4 s_p[kRansacMaxPts];
+  extern __shared__ __attribute__((aligned(16))) double s_pd[];  // [n][4]
   const int p = blockIdx.y;
   const int n = npts[p];
   const int4* P = reinterpret_cast<const int4*>(pts + (int64_t)p * nmax * 4);
-  for (int i = threadIdx.x; i < n; i += 256) s_p[i] = P[i];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int per_block = (iters + gridDim.x - 1) / gridDim.x;
-  const int it0 = blockIdx.x * per_block, it1 = min(iters, it0 + per_block);
-  for (int it = it0 + wv; it < it1; it += 4) {
-    const double* F = Fs + ((int64_t)p * iters + it) * 9;
-    double f[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) f[k] = F[k];
-    uint32_t c = 0;
-    for (int i = lane; i < n; i += 64) {
-      const int4 q = s_p[i];
-      c += epi_inlier(f, (double)q.x, (double)q.y, (double)q.z, (double)q.w, thr) ? 1u : 0u;
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
-    if (lane == 0) counts[(int64_t)p * iters + it] = n < 8 ? 0 : (int32_t)c;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const int4 q = P[i];
+    s_pd[4 * i + 0] = (double)q.x;
+    s_pd[4 * i + 1] = (double)q.y;
+    s_pd[4 * i + 2] = (double)q.z;
+    s_pd[4 * i + 3] = (double)q.w;
   }
+  __syncthreads();
+  const int it = blockIdx.x * 256 + threadIdx.x;
+  if (it >= iters) return;
+  const double* F = Fs + ((int64_t)p * iters + it) * 9;
+  double f[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) f[k] = F[k];
+  const EpiThr t = epi_thr(thr);
+  uint32_t c = 0;
+  for (int i = 0; i < n; ++i) {
+    const double4 q = reinterpret_cast<const double4*>(s_pd)[i];
+    c += epi_inlier(f, q.x, q.y, q.z, q.w, t.thr, t.lo, t.hi) ? 1u : 0u;
+  }
+  counts[(int64_t)p * iters + it] = n < 8 ? 0 : (int32_t)c;
 }
 
 // per pair: the first sample with the most inliers, its inliers compacted in order
@@ -435,6 +451,7 @@ __global__ void __launch_bounds__(256) k_ransac_select(const int32_t* __restrict
   const double* F = Fs + ((int64_t)p * iters + best) * 9;
   const int4* P = reinterpret_cast<const int4*>(pts + (int64_t)p * nmax * 4);
   int4* O = reinterpret_cast<int4*>(out_pts + (int64_t)p * nmax * 4);
+  const EpiThr t = epi_thr(thr);  // the same test as k_ransac_count, so the mask has the count
   uint32_t base = 0;
   for (int i0 = 0; i0 < n; i0 += 256) {
     const int i = i0 + tid;
@@ -442,7 +459,7 @@ __global__ void __launch_bounds__(256) k_ransac_select(const int32_t* __restrict
     int4 q = make_int4(0, 0, 0, 0);
     if (i < n) {
       q = P[i];
-      in = epi_inlier(F, (double)q.x, (double)q.y, (double)q.z, (double)q.w, thr);
+      in = epi_inlier(F, (double)q.x, (double)q.y, (double)q.z, (double)q.w, t.thr, t.lo, t.hi);
     }
     uint32_t total;
     const uint32_t pos = block_exclusive_scan(in ? 1u : 0u, s_scan, &total);
@@ -457,8 +474,13 @@ void launch_ransac(const int32_t* pts, const int32_t* npts, int nmax, int P, con
                    int32_t* out_n, int32_t* out_iter, hipStream_t st) {
   hipLaunchKernelGGL(k_ransac_F, dim3((iters + 127) / 128, P), dim3(128), 0, st, pts, npts, nmax, idx, idx_off,
                      iters, Fs);
-  const int blocks = std::max(1, std::min(64, (iters + 63) / 64));
-  hipLaunchKernelGGL(k_ransac_count, dim3(blocks, P), dim3(256), 0, st, pts, npts, nmax, Fs, iters, thr, counts);
+  static const bool lds_attr = [] {  // up to kRansacMaxPts x 32 B of staged points
+    return hipFuncSetAttribute((const void*)k_ransac_count, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               kRansacMaxPts * 32) == hipSuccess;
+  }();
+  (void)lds_attr;
+  hipLaunchKernelGGL(k_ransac_count, dim3((iters + 255) / 256, P), dim3(256), (size_t)nmax * 32, st, pts, npts, nmax,
+                     Fs, iters, thr, counts);
   hipLaunchKernelGGL(k_ransac_select, dim3(P), dim3(256), 0, st, pts, npts, nmax, Fs, counts, iters, thr, out_pts,
                      out_n, out_iter);
 }
