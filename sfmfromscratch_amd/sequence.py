@@ -14,10 +14,11 @@ ThreadPool's Python work serialises on the GIL.  Here:
 * `stage1` mirrors what SFMRunner.perform leaves in `all_matches` after its thread pool:
   `all_matches[i1][i2] = Matches(matches, confidences, p1, p2, K1, K2)` and the swapped
   entry `[i2][i1]` (Runner.py:354-355), with p1 / p2 from _convert_matches_to_coords
-  (Runner.py:423-434, first 2,500 matches).  The pose side — EXIF intrinsics
-  (CameraPose.construct_K) and the RANSAC inlier filter applied to pairs other than
-  (1, 2) (Runner.py:349-351) — is out of scope: K is the caller's
-  `single_K` (or None) and p1 / p2 are the pre-RANSAC correspondences.
+  (Runner.py:423-434, first 2,500 matches).  With `ransac=True` the RANSAC inlier
+  filter the reference applies to every pair but (1, 2) (Runner.py:349-351) runs on the
+  device for all pairs at once (pose.find_inliers_batch); otherwise p1 /
+  p2 are the pre-RANSAC correspondences.  EXIF intrinsics (CameraPose.construct_K) are
+  out of scope: K is the caller's `single_K` (or None).
 
 Feature tables and matches are saved / loaded as .npz (the
 reference's own output format is np.savez, Runner.py:357-359).
