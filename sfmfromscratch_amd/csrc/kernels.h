@@ -151,6 +151,9 @@ int ingest_rows_ks(int ks_h, int ks_v);
 void launch_ingest_rgb(const uint8_t* rgb, uint8_t* tmp, float* gray, const int32_t* tab_h, int ks_h,
                        const int32_t* tab_v, int ks_v, const int32_t* colmap, const int32_t* sets, int nsets,
                        int B, int H, int W, int H2, int W2, hipStream_t st);
+// levels l+1..l+3 of exact 2x steps in one pass; false (nothing launched) when the sizes or
+// alignments do not allow it
+bool launch_down2x3(const float* src, int sh, int sw, float* d1, float* d2, float* d3, int B, hipStream_t st);
 void launch_resize(const float* src, int sh, int sw, float* dst, int dh, int dw, int B,
                    hipStream_t st);
 

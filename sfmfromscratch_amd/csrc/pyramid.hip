@@ -10,6 +10,8 @@
 
 namespace sfm {
 
+static int grid_for(int64_t n, int per_thread);
+
 // uint8 -> float32 value/255 (Runner.py:521).  4 pixels per thread, 16-byte stores.
 __global__ void __launch_bounds__(256) k_u8_to_f32(const uint8_t* __restrict__ src,
                                                    float* __restrict__ dst, int64_t n) {
@@ -53,6 +55,70 @@ __global__ void __launch_bounds__(256) k_down2(const float* __restrict__ src, in
       d[x + 1] = (t0 + t1) * 0.25f;
     }
   }
+}
+
+// Three exact 2x levels in one pass (level l -> l+1, l+2, l+3): each thread reads one
+// 8 x 8 block of level l with 16-B loads and writes its 4 x 4, 2 x 2 and 1 x 1 blocks,
+// every value ((a00 + a01) + (a10 + a11)) * 0.25 of the level above, exactly k_down2's
+// expression, so the levels are bit-identical to three k_down2 launches — without
+// re-reading levels l+1 and l+2.  Needs sh, sw divisible by 8 and 16-B aligned planes.
+SFM_DEV float down2_px(float a00, float a01, float a10, float a11) {
+  const float t0 = a00 + a01;
+  const float t1 = a10 + a11;
+  return (t0 + t1) * 0.25f;
+}
+
+__global__ void __launch_bounds__(256) k_down2x3(const float* __restrict__ src, int sh, int sw,
+                                                 float* __restrict__ d1, float* __restrict__ d2,
+                                                 float* __restrict__ d3, int B) {
+  const int bw = sw >> 3, bh = sh >> 3;
+  const int w1 = sw >> 1, w2 = sw >> 2, w3 = sw >> 3;
+  const int h1 = sh >> 1, h2 = sh >> 2, h3 = sh >> 3;
+  const int64_t total = (int64_t)B * bh * bw;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int bx = (int)(t % bw);
+    const int64_t r = t / bw;
+    const int by = (int)(r % bh);
+    const int b = (int)(r / bh);
+    const float* s = src + ((int64_t)b * sh + 8 * by) * sw + 8 * bx;
+    float a[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float4 lo = *reinterpret_cast<const float4*>(s + (int64_t)i * sw);
+      const float4 hi = *reinterpret_cast<const float4*>(s + (int64_t)i * sw + 4);
+      a[i][0] = lo.x; a[i][1] = lo.y; a[i][2] = lo.z; a[i][3] = lo.w;
+      a[i][4] = hi.x; a[i][5] = hi.y; a[i][6] = hi.z; a[i][7] = hi.w;
+    }
+    float l1[4][4], l2[2][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        l1[i][j] = down2_px(a[2 * i][2 * j], a[2 * i][2 * j + 1], a[2 * i + 1][2 * j], a[2 * i + 1][2 * j + 1]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        l2[i][j] = down2_px(l1[2 * i][2 * j], l1[2 * i][2 * j + 1], l1[2 * i + 1][2 * j], l1[2 * i + 1][2 * j + 1]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<float4*>(d1 + ((int64_t)b * h1 + 4 * by + i) * w1 + 4 * bx) =
+          make_float4(l1[i][0], l1[i][1], l1[i][2], l1[i][3]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      *reinterpret_cast<float2*>(d2 + ((int64_t)b * h2 + 2 * by + i) * w2 + 2 * bx) = make_float2(l2[i][0], l2[i][1]);
+    d3[((int64_t)b * h3 + by) * w3 + bx] = down2_px(l2[0][0], l2[0][1], l2[1][0], l2[1][1]);
+  }
+}
+
+bool launch_down2x3(const float* src, int sh, int sw, float* d1, float* d2, float* d3, int B, hipStream_t st) {
+  const bool ok = sh % 8 == 0 && sw % 8 == 0 && sh >= 8 && sw >= 8 && ((uintptr_t)src & 15) == 0 &&
+                  ((uintptr_t)d1 & 15) == 0 && ((uintptr_t)d2 & 7) == 0;
+  if (!ok) return false;
+  const int64_t n = (int64_t)B * (sh / 8) * (sw / 8);
+  hipLaunchKernelGGL(k_down2x3, dim3(grid_for(n, 1)), dim3(256), 0, st, src, sh, sw, d1, d2, d3, B);
+  return true;
 }
 
 struct LinCoef {

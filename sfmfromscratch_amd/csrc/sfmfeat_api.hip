@@ -246,9 +246,21 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     int64_t off = 0;
     for (int l = 1; l < L; ++l) {
       float* dst = as<float>(c->d_lvl) + off;
-      launch_resize(lvl[l - 1], lv[l - 1].h, lv[l - 1].w, dst, lv[l].h, lv[l].w, B, st);
       lvl[l] = dst;
       off += (int64_t)B * lv[l].h * lv[l].w;
+    }
+    for (int l = 1; l < L;) {
+      // three exact 2x levels from one read of their source where the sizes allow
+      const auto& s = lv[l - 1];
+      const bool x2 = l + 2 < L && lv[l].h * 2 == s.h && lv[l].w * 2 == s.w && lv[l + 1].h * 4 == s.h &&
+                      lv[l + 1].w * 4 == s.w && lv[l + 2].h * 8 == s.h && lv[l + 2].w * 8 == s.w;
+      if (x2 && launch_down2x3(lvl[l - 1], s.h, s.w, const_cast<float*>(lvl[l]), const_cast<float*>(lvl[l + 1]),
+                               const_cast<float*>(lvl[l + 2]), B, st)) {
+        l += 3;
+        continue;
+      }
+      launch_resize(lvl[l - 1], s.h, s.w, const_cast<float*>(lvl[l]), lv[l].h, lv[l].w, B, st);
+      ++l;
     }
   }
   HIPCHK(c, hipMemsetAsync(c->d_hist.p, 0, (size_t)L * B * kMedBins1 * 4, st));
