@@ -149,7 +149,8 @@ int32_t sfm_resize_dims(int32_t H, int32_t W, double scale, int32_t* H2, int32_t
  * coordinates (the pairs of _convert_matches_to_coords, Runner.py:423-434); iters =
  * max_iterations; samples replay numpy's legacy RandomState after np.random.seed(5).
  * in1 / in2 (capacity n x 2) receive the winning sample's inliers in input order,
- * n_out their count; n_out = -1 when n < 8 (the reference returns four Nones).
+ * n_out their count; n_out = -1 when n < 8 (the reference returns four Nones), 0 when
+ * iters == 0 (the reference's empty arrays).  No limit on n.
  * best_iter (optional): the winning sample's index.
  */
 int32_t sfm_ransac_find_inliers(sfm_ctx* ctx, const int64_t* p1, const int64_t* p2, int64_t n, int32_t iters,
@@ -179,8 +180,9 @@ int32_t sfm_reserve(sfm_ctx* ctx, int32_t B, int32_t H, int32_t W);
 
 /* sfm_ransac_find_inliers for P pairs at once: pts [P][nmax][4] int32 (x1, y1, x2, y2),
  * npts [P] on the device and npts_host [P] on the host (the sample streams depend on n);
- * out_pts [P][nmax][4] inliers in order, out_n [P] (-1 for n < 8), out_iter [P].
- * nmax <= 2560.  Synchronises the stream before returning. */
+ * out_pts [P][nmax][4] inliers in order, out_n [P] (-1 for n < 8, 0 when iters == 0),
+ * out_iter [P] (-1 when no sample won).  Any nmax (the points are staged through LDS in
+ * chunks).  Synchronises the stream before returning. */
 int32_t sfm_ransac_find_inliers_dev(sfm_ctx* ctx, const int32_t* pts, const int32_t* npts,
                                     const int32_t* npts_host, int32_t P, int32_t nmax, int32_t iters,
                                     double threshold, int32_t* out_pts, int32_t* out_n, int32_t* out_iter,

@@ -136,7 +136,6 @@ void launch_u8_to_f32(const uint8_t* src, float* dst, int64_t n, hipStream_t st)
 // ransac.hip: CameraPose.find_inliers (SFM.py:126-160) for P correspondence sets
 // pts [P][nmax][4] int32 (x1, y1, x2, y2), sample indices idx (+ idx_off[p]) [iters][8].
 void ransac_sample_indices(int n, int iters, uint32_t seed, int32_t* out);
-int ransac_max_points();
 void launch_ransac(const int32_t* pts, const int32_t* npts, int nmax, int P, const int32_t* idx,
                    const int32_t* idx_off, int iters, double thr, double* Fs, int32_t* counts, int32_t* out_pts,
                    int32_t* out_n, int32_t* out_iter, hipStream_t st);

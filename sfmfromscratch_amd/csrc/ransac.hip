@@ -383,38 +383,46 @@ SFM_DEV EpiThr epi_thr(double thr) {  // thr <= 0 (or NaN): nothing is an inlier
 }
 
 // inlier count per (pair, sample): one thread per sample, its F in registers for the whole
-// sweep; the pair's points are staged in LDS as float64 (x1, y1, x2, y2) and every lane
-// reads the same point (a broadcast) — no per-sample reduction, F reload or conversion
-constexpr int kRansacMaxPts = 2560;
+// sweep; the pair's points are staged in LDS as float64 (x1, y1, x2, y2) in chunks of
+// kRansacChunk points and every lane reads the same point (a broadcast) — no per-sample
+// reduction, F reload or conversion.  Any n: larger sets take several chunks.
+constexpr int kRansacChunk = 2560;
 __global__ void __launch_bounds__(256) k_ransac_count(const int32_t* __restrict__ pts,
                                                       const int32_t* __restrict__ npts, int nmax,
                                                       const double* __restrict__ Fs, int iters, double thr,
                                                       int32_t* __restrict__ counts) {
-  extern __shared__ __attribute__((aligned(16))) double s_pd[];  // [n][4]
+  extern __shared__ __attribute__((aligned(16))) double s_pd[];  // [chunk][4]
   const int p = blockIdx.y;
   const int n = npts[p];
   const int4* P = reinterpret_cast<const int4*>(pts + (int64_t)p * nmax * 4);
-  for (int i = threadIdx.x; i < n; i += 256) {
-    const int4 q = P[i];
-    s_pd[4 * i + 0] = (double)q.x;
-    s_pd[4 * i + 1] = (double)q.y;
-    s_pd[4 * i + 2] = (double)q.z;
-    s_pd[4 * i + 3] = (double)q.w;
-  }
-  __syncthreads();
   const int it = blockIdx.x * 256 + threadIdx.x;
-  if (it >= iters) return;
-  const double* F = Fs + ((int64_t)p * iters + it) * 9;
+  const bool live = it < iters;
   double f[9];
+  if (live) {
+    const double* F = Fs + ((int64_t)p * iters + it) * 9;
 #pragma unroll
-  for (int k = 0; k < 9; ++k) f[k] = F[k];
+    for (int k = 0; k < 9; ++k) f[k] = F[k];
+  }
   const EpiThr t = epi_thr(thr);
   uint32_t c = 0;
-  for (int i = 0; i < n; ++i) {
-    const double4 q = reinterpret_cast<const double4*>(s_pd)[i];
-    c += epi_inlier(f, q.x, q.y, q.z, q.w, t.thr, t.lo, t.hi) ? 1u : 0u;
+  for (int i0 = 0; i0 < n; i0 += kRansacChunk) {
+    const int m = min(kRansacChunk, n - i0);
+    if (i0) __syncthreads();  // every lane is done with the previous chunk
+    for (int i = threadIdx.x; i < m; i += 256) {
+      const int4 q = P[i0 + i];
+      s_pd[4 * i + 0] = (double)q.x;
+      s_pd[4 * i + 1] = (double)q.y;
+      s_pd[4 * i + 2] = (double)q.z;
+      s_pd[4 * i + 3] = (double)q.w;
+    }
+    __syncthreads();
+    if (live)
+      for (int i = 0; i < m; ++i) {
+        const double4 q = reinterpret_cast<const double4*>(s_pd)[i];
+        c += epi_inlier(f, q.x, q.y, q.z, q.w, t.thr, t.lo, t.hi) ? 1u : 0u;
+      }
   }
-  counts[(int64_t)p * iters + it] = n < 8 ? 0 : (int32_t)c;
+  if (live) counts[(int64_t)p * iters + it] = n < 8 ? 0 : (int32_t)c;
 }
 
 // per pair: the first sample with the most inliers, its inliers compacted in order
@@ -472,19 +480,21 @@ __global__ void __launch_bounds__(256) k_ransac_select(const int32_t* __restrict
 void launch_ransac(const int32_t* pts, const int32_t* npts, int nmax, int P, const int32_t* idx,
                    const int32_t* idx_off, int iters, double thr, double* Fs, int32_t* counts, int32_t* out_pts,
                    int32_t* out_n, int32_t* out_iter, hipStream_t st) {
-  hipLaunchKernelGGL(k_ransac_F, dim3((iters + 127) / 128, P), dim3(128), 0, st, pts, npts, nmax, idx, idx_off,
-                     iters, Fs);
-  static const bool lds_attr = [] {  // up to kRansacMaxPts x 32 B of staged points
-    return hipFuncSetAttribute((const void*)k_ransac_count, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               kRansacMaxPts * 32) == hipSuccess;
-  }();
-  (void)lds_attr;
-  hipLaunchKernelGGL(k_ransac_count, dim3((iters + 255) / 256, P), dim3(256), (size_t)nmax * 32, st, pts, npts, nmax,
-                     Fs, iters, thr, counts);
+  if (iters > 0) {
+    hipLaunchKernelGGL(k_ransac_F, dim3((iters + 127) / 128, P), dim3(128), 0, st, pts, npts, nmax, idx, idx_off,
+                       iters, Fs);
+    static const bool lds_attr = [] {  // up to kRansacChunk x 32 B of staged points
+      return hipFuncSetAttribute((const void*)k_ransac_count, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 kRansacChunk * 32) == hipSuccess;
+    }();
+    (void)lds_attr;
+    hipLaunchKernelGGL(k_ransac_count, dim3((iters + 255) / 256, P), dim3(256),
+                       (size_t)std::min(nmax, kRansacChunk) * 32, st, pts, npts, nmax, Fs, iters, thr, counts);
+  }
+  // always: with iters == 0 no sample exists and every pair gets the reference's empty
+  // result (n >= 8) or None (n < 8), out_iter -1
   hipLaunchKernelGGL(k_ransac_select, dim3(P), dim3(256), 0, st, pts, npts, nmax, Fs, counts, iters, thr, out_pts,
                      out_n, out_iter);
 }
-
-int ransac_max_points() { return kRansacMaxPts; }
 
 }  // namespace sfm

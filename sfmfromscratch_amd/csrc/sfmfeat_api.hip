@@ -693,7 +693,6 @@ void ransac_prefetch_streams(sfm_ctx* c, const std::vector<int>& ns, int iters) 
 
 int ransac_impl(sfm_ctx* c, const int32_t* pts, const int32_t* npts_dev, const int32_t* npts_host, int P, int nmax,
                 int iters, double thr, int32_t* out_pts, int32_t* out_n, int32_t* out_iter, hipStream_t st) {
-  if (nmax > ransac_max_points()) return set_err(c, SFM_EINVAL, "more than 2560 correspondences per pair");
   // sample streams (host replay of numpy's RandomState; identical for equal n)
   {
     std::vector<int> ns;
@@ -755,7 +754,7 @@ int32_t sfm_ransac_find_inliers_dev(sfm_ctx* c, const int32_t* pts, const int32_
 int32_t sfm_ransac_find_inliers(sfm_ctx* c, const int64_t* p1, const int64_t* p2, int64_t n, int32_t iters,
                                 double threshold, int64_t* in1, int64_t* in2, int64_t* n_out, int32_t* best_iter) {
   if (!c || !n_out || n < 0 || iters < 0 || (n > 0 && (!p1 || !p2))) return SFM_EINVAL;
-  if (n > ransac_max_points()) return set_err(c, SFM_EINVAL, "more than 2560 correspondences");
+  if (n > INT32_MAX / 4) return set_err(c, SFM_EINVAL, "too many correspondences");
   HIPCHK(c, hipSetDevice(c->device));
   *n_out = -1;
   if (n < 8) return SFM_OK;  // the reference returns (None, None, None, None)
@@ -784,6 +783,7 @@ int32_t sfm_ransac_find_inliers(sfm_ctx* c, const int64_t* p1, const int64_t* p2
   HIPCHK(c, hipMemcpyAsync(&k, c->r_on.p, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipMemcpyAsync(&bi, c->r_oit.p, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(c, hipStreamSynchronize(st));
+  if (k > n) return set_err(c, SFM_EDEVICE, "inlier count above the correspondence count");
   if (k > 0) {
     std::vector<int32_t> o((size_t)k * 4);
     HIPCHK(c, hipMemcpy(o.data(), c->r_out.p, o.size() * 4, hipMemcpyDeviceToHost));

@@ -165,6 +165,9 @@ class BatchPipeline:
         ln = self.lanes[self.n % self.inflight]
         self.n += 1
         ln["stream"].wait_stream(torch.cuda.current_stream(frames.device))
+        # the lane reads `frames` after the caller may have dropped it: keep its memory
+        # out of the caching allocator until the lane's work is done
+        frames.record_stream(ln["stream"])
         with torch.cuda.stream(ln["stream"]):
             ln["ex"].extract(frames, out=ln["view"])
             if hook is not None:

@@ -65,8 +65,12 @@ def find_inliers_batch(pairs, threshold=1.0, max_iterations=1000, device: int = 
         a, b = np.asarray(a), np.asarray(b)
         if len(a) < 8:
             res[k] = (None, None, None, None)
-        else:
-            todo.append((k, a, b))
+            continue
+        if not (np.array_equal(a, np.round(a)) and np.array_equal(b, np.round(b))):
+            raise ValueError(f"pair {k}: find_inliers takes integer pixel coordinates (Runner.py:423-434)")
+        if a.shape != b.shape or a.ndim != 2 or a.shape[1] != 2:
+            raise ValueError(f"pair {k}: p1 and p2 must both be [n, 2]")
+        todo.append((k, a, b))
     if not todo:
         return res
     nmax = max(len(a) for _, a, _ in todo)

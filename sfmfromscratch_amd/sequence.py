@@ -82,7 +82,20 @@ class FeatureCache:
         self.n = n
         self.slots = SlotTable(torch, max(n, 1), self.cap, dev)
         self.shapes = [None] * n
-        loaded = [load_image_u8(f) if isinstance(f, str) else np.asarray(f) for f in frames]
+        loaded = []
+        for f in frames:
+            if isinstance(f, str):
+                a = load_image_u8(f)
+                # the reference's _rgb2gray indexes three channels (Runner.py:478): a gray
+                # or RGBA file fails there, so it fails here instead of being extracted at
+                # the wrong scale
+                if a.ndim != 3 or a.shape[2] != 3 or a.dtype != np.uint8:
+                    raise ValueError(f"{f}: the reference's _rgb2gray needs an [H, W, 3] RGB frame")
+            else:
+                a = np.asarray(f)
+                if a.ndim == 2 and a.dtype != np.float32:
+                    raise ValueError("gray frames must be float32 [H, W] in [0, 1] (the extractor's input)")
+            loaded.append(a)
         # group frames of one kind and size into batches (one launch sequence per batch)
         groups: dict = {}
         for i, a in enumerate(loaded):
@@ -98,7 +111,7 @@ class FeatureCache:
                         raise ValueError("RGB frames must be [H, W, 3] uint8")
                     gray = ingest_rgb(self.extractor.ctx, t, scale_factor)
                 elif t.dim() == 3:
-                    gray = t.float() if t.dtype != torch.uint8 else t
+                    gray = t
                 else:
                     raise ValueError("frames must be [H, W, 3] uint8 RGB or [H, W] gray")
                 sel = torch.tensor(chunk, device=dev)

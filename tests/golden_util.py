@@ -113,12 +113,25 @@ def assert_matches_equal(m_ref, c_ref, m, c):
 # that ulp-level noise into up to ~1e-4 absolute.  Such elements are compared in the
 # squared (pre-sqrt, L2-normalised) domain, where the reference's own ambiguity is
 # <= 2e-6 (verified: with a stable argsort the reference equals the oracle there).
+# The escape is narrow on purpose: only near-empty bins (|ref| < DESC_SQ_MAXREF) and at
+# most DESC_MAX_ESCAPES elements per table.  Measured on every fixture: one element in
+# total (extract_small_pmain.npz frame 1: ref 2.6e-4, |diff| 7.7e-5); everything else is
+# within 1e-4 relative, so a real regression in any bin fails.
 DESC_SQ_ATOL = 2e-6
+DESC_SQ_MAXREF = 1e-3
+DESC_MAX_ESCAPES = 1
 
 
-def desc_close(ref, got, rtol=DESC_RTOL, atol=DESC_ATOL):
+def desc_close(ref, got, rtol=DESC_RTOL, atol=DESC_ATOL, max_escapes=DESC_MAX_ESCAPES):
     ref = np.asarray(ref, np.float32)
     got = np.asarray(got, np.float32)
+    if ref.shape != got.shape:
+        return False
     ok = np.abs(ref - got) <= atol + rtol * np.abs(ref)
-    ok |= np.abs(ref.astype(np.float64) ** 2 - got.astype(np.float64) ** 2) <= DESC_SQ_ATOL
-    return bool(np.all(ok))
+    esc = ~ok
+    if not esc.any():
+        return True
+    if int(esc.sum()) > max_escapes:
+        return False
+    r, g = ref[esc].astype(np.float64), got[esc].astype(np.float64)
+    return bool(np.all((np.abs(r) < DESC_SQ_MAXREF) & (np.abs(r ** 2 - g ** 2) <= DESC_SQ_ATOL)))

@@ -69,3 +69,43 @@ def test_batch_dev_api_matches_host_api():
         k = int(on[p])
         assert k == len(r[0])
         assert np.array_equal(op[p, :k, :2], r[0]) and np.array_equal(op[p, :k, 2:], r[1])
+
+
+def test_zero_iterations_after_a_call_with_inliers():
+    """max_iterations=0: the reference's loop never runs and it returns two empty arrays;
+    the result must not be the previous call's (stale device counters)."""
+    z = load("ransac.npz")
+    p1, p2 = z["c0_p1"], z["c0_p2"]
+    r = pose.find_inliers(p1, p2, max_iterations=200)
+    assert len(r[0]) > 0
+    r0 = pose.find_inliers(p1, p2, max_iterations=0)
+    assert len(r0) == 2 and r0[0].shape == (0,) and r0[1].shape == (0,)
+    rb = pose.find_inliers_batch([(p1, p2), (p1[:7], p2[:7]), (p1, p2)], max_iterations=0)
+    assert rb[1] == (None, None, None, None)
+    for k in (0, 2):
+        assert rb[k][0].shape == (0,) and rb[k][1].shape == (0,)
+    o = R.find_inliers(p1, p2, 1.0, 0)
+    assert len(o[0]) == 0
+
+
+def test_more_points_than_one_lds_chunk_vs_oracle():
+    """n = 4000 > the 2560-point LDS chunk of k_ransac_count (the reference has no limit)."""
+    rng = np.random.default_rng(7)
+    n = 4000
+    p1 = rng.integers(0, 1900, (n, 2)).astype(np.int64)
+    p2 = p1 + np.array([4, 2])
+    out = rng.random(n) > 0.55
+    p2[out] = rng.integers(0, 1900, (int(out.sum()), 2))
+    r = pose.find_inliers(p1, p2, max_iterations=150)
+    o = R.find_inliers(p1, p2, 1.0, 150)
+    assert np.array_equal(r[0], o[0]) and np.array_equal(r[1], o[1])
+    rb = pose.find_inliers_batch([(p1, p2), (p1[:900], p2[:900])], max_iterations=150)
+    assert np.array_equal(rb[0][0], o[0]) and np.array_equal(rb[0][1], o[1])
+    o2 = R.find_inliers(p1[:900], p2[:900], 1.0, 150)
+    assert np.array_equal(rb[1][0], o2[0]) and np.array_equal(rb[1][1], o2[1])
+
+
+def test_batch_rejects_float_coordinates():
+    p = np.arange(40, dtype=np.float64).reshape(20, 2)
+    with pytest.raises(ValueError):
+        pose.find_inliers_batch([(p + 0.5, p)], max_iterations=10)
