@@ -98,16 +98,27 @@ def cpu_baseline(frames_per_thread: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=2,
                     help="frames per host thread in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="disable the live per-stage HIP events")
-    ap.add_argument("--workload", choices=["c2", "c3", "c5"], default="c2",
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2 = BASELINE configs[1] (the headline line); c3 = configs[2] (256 frames, all "
-                         "pairs); c5 = configs[4]'s per-GPU share (4K, 5 octaves, k 8000)")
-    ap.add_argument("--frames", type=int, default=256, help="c3: frames in the all-pairs job")
+                         "pairs); c4 = configs[3] (2048 frames sharded over the ranks, chunked RCCL all-gather "
+                         "of the descriptor tables, pairwise match); c5 = configs[4]'s per-GPU share (4K, "
+                         "5 octaves, k 8000)")
+    ap.add_argument("--frames", type=int, default=None,
+                    help="c3: frames in the all-pairs job (256); c4: global frames (strong: 2048) or frames "
+                         "per GPU (weak: 256)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="c4: fixed global frame count (strong) or fixed frames per GPU (weak)")
+    ap.add_argument("--pairs", default="consecutive",
+                    help="c4 pair schedule: consecutive | window:W | all")
+    ap.add_argument("--exchange", choices=["allgather", "halo"], default="allgather",
+                    help="c4: chunked all-gather of every slot table (configs[3]) or, for consecutive pairs, "
+                         "only the 1-slot point-to-point halo")
     ap.add_argument("--rgb-ingest", action="store_true",
                     help="c2: frames resident as decoded 2x-size RGB (3840x2160x3 u8); each step first runs "
                          "FeatureRunner's ingest on the device (PIL BICUBIC x0.5 + _rgb2gray, Runner.py:33-46)")
@@ -128,6 +139,8 @@ def main():
 
     if args.workload == "c3":
         return run_all_pairs(args, torch, dev)
+    if args.workload == "c4":
+        return run_gather(args, torch, dist, dev, rank, world)
     if args.workload == "c5":
         global H, W, P_OCT
         H, W = 2160, 3840
@@ -182,18 +195,24 @@ def main():
     torch.cuda.synchronize()
 
     def stage_work(counts, nsteps):
-        """Algorithmic work of `nsteps` steps per stage: (bound, amount, unit, peak)."""
+        """Algorithmic work of `nsteps` steps per stage:
+        (bound, amount, unit, peak, algorithmic HBM bytes or None).  Latency-bound stages
+        (describe, top-k, median) get no roofline."""
         levels = [(H >> l, W >> l) for l in range(P_OCT["pyramid_level"])]
         px = sum(h * w for h, w in levels) * B * nsteps
-        px_lo = sum(h * w for h, w in levels[1:]) * B * nsteps
         pair_elems = sum(int(counts[i]) * int(counts[j]) for i, j in pairs_np) * 128 * nsteps
-        kps = int(counts[:B].sum()) * nsteps
+        # k_down2x3 reads level 0 once and writes levels 1..3 (one launch); a 5th level is
+        # one k_down2 from level 3
+        A = [h * w for h, w in levels]
+        pyr_px = A[0] + sum(A[1:4]) + sum(A[l - 1] + A[l] for l in range(4, len(A)))
+        pyr_bytes = 4.0 * pyr_px * B * nsteps
         return {
-            "harris": ("mfma", HARRIS_FLOP_PER_PX * px / 1e12, "TFLOP/s", PEAK_F32_TFLOPS),
-            "match": ("mfma", MATCH_FLOP_PER_ELEM * pair_elems / 1e12, "TFLOP/s", PEAK_MATCH_TFLOPS),
-            "nms": ("hbm", 4.0 * px / 1e9, "GB/s", PEAK_HBM_GBS),          # one read of R
-            "pyramid": ("hbm", 4.0 * px_lo * 5 / 1e9, "GB/s", PEAK_HBM_GBS),  # read 4 px, write 1
-            "describe": ("hbm", DESC_BYTES_PER_KP * kps / 1e9, "GB/s", PEAK_HBM_GBS),
+            # VALU-bound (SURVEY.md §8d): 328 flop/px of separate mul/add-class ops; bytes: read
+            # the level, write R
+            "harris": ("valu", HARRIS_FLOP_PER_PX * px / 1e12, "TFLOP/s", PEAK_F32_TFLOPS, 8.0 * px),
+            "match": ("mfma", MATCH_FLOP_PER_ELEM * pair_elems / 1e12, "TFLOP/s", PEAK_MATCH_TFLOPS, None),
+            "nms": ("hbm", 4.0 * px / 1e9, "GB/s", PEAK_HBM_GBS, 4.0 * px),          # one read of R
+            "pyramid": ("hbm", pyr_bytes / 1e9, "GB/s", PEAK_HBM_GBS, pyr_bytes),
         }
 
     def prof_enable(on):
@@ -230,7 +249,7 @@ def main():
                 continue
             st = {"ms_per_step": round(ms / nprof, 4), "launches_per_step": n // nprof}
             if k in work:
-                bound, amount, unit, peak = work[k]
+                bound, amount, unit, peak, _ = work[k]
                 ach = amount / (ms / 1e3)
                 st.update({"bound": bound, "achieved": round(ach, 3), "unit": unit, "frac": round(ach / peak, 4)})
             stages[k] = st
@@ -275,13 +294,16 @@ def main():
         if os.path.exists(TRAFFIC_FILE):
             with open(TRAFFIC_FILE) as f:
                 traffic = json.load(f).get("bytes_per_launch", {})
-        bound, amount, unit, peak = stage_work(counts, args.steps)[dom]
+        bound, amount, unit, peak, abytes = stage_work(counts, args.steps)[dom]
         ms, n = prof[dom]
         achieved = amount / (ms / 1e3)
         kname = KERNELS[dom]
         tr = traffic.get(kname)
+        alg_per_launch = abytes / max(n, 1) if abytes else None
         roof = {"kernel": kname, "stage": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak,
                 "unit": unit, "frac": round(achieved / peak, 4), "traffic": tr,
+                "algorithmic_bytes_per_launch": round(alg_per_launch) if alg_per_launch else None,
+                "traffic_ratio": round(tr / alg_per_launch, 3) if tr and alg_per_launch else None,
                 "avg_launch_ms": round(ms / max(n, 1), 4), "launches": n,
                 "timing": "HIP events around each launch of the stage inside the timed region "
                           f"({args.inflight} batches in flight)"}
@@ -336,7 +358,7 @@ def run_all_pairs(args, torch, dev):
     split-f16 MFMA prefilter + exact f32 re-rank).  One step = the whole job."""
     from sfmfromscratch_amd import synth
     from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, SlotTable, all_pairs
-    N, Bx = args.frames, 32
+    N, Bx = args.frames or 256, 32
     host = np.stack([synth.make_frame_u8(H, W, 1234 + 1000 * (i // 32), i % 32) for i in range(N)])
     frames = torch.from_numpy(synth.u8_to_gray(host)).to(dev)
     del host
@@ -370,8 +392,10 @@ def run_all_pairs(args, torch, dev):
                 ex.extract(frames[b0:b0 + Bx], out=v)
         for _, stm in lanes:
             cur.wait_stream(stm)
+        matcher.prep(slots)  # operands of every slot once, then the pair chunks
         for a in range(0, P, CH):
-            matcher.match(slots, pairs[a:a + CH], out=(out[0][a:a + CH], out[1][a:a + CH], out[2][a:a + CH]))
+            matcher.match(slots, pairs[a:a + CH], out=(out[0][a:a + CH], out[1][a:a + CH], out[2][a:a + CH]),
+                          prepped=True)
 
     for _ in range(args.warmup):
         step()
@@ -413,6 +437,230 @@ def run_all_pairs(args, torch, dev):
                      "note": "GEMM-equivalent 2*n1*n2*128 flop per pair (SURVEY.md §8d) against the split-f16 "
                              "MFMA bound 2500/3 TFLOP/s"},
         "cpu_baseline": None}), flush=True)
+
+
+def run_gather(args, torch, dist, dev, rank, world):
+    """BASELINE configs[3]: n_global 1080p frames sharded over the ranks (rank r owns
+    [r*S, (r+1)*S)), each shard extracted in 32-frame chunks with --inflight chunks on the
+    GPU at once; every chunk's slot table (xy, desc, count; fixed capacity) is all-gathered
+    over RCCL as soon as it is extracted (distributed.GatherPlan: chunk-major global
+    table), so the gather of chunk c overlaps the extraction of chunk c+1, and the pairs
+    that become ready with chunk c are matched on their own stream while later chunks are
+    still being extracted.  One step = the whole job: every frame extracted once, the
+    rank's pairs matched.  --exchange halo replaces the all-gather by the 1-slot
+    point-to-point halo (consecutive pairs only need rank r+1's first frame).
+
+    strong scaling: n_global fixed (default 2048) for every world size; weak: 256 frames
+    per GPU.  Frames are device-resident uint8 (the u8 -> f32 gray conversion runs inside
+    extraction), tiled from up to 64 distinct synthetic frames per rank to bound host
+    generation time."""
+    from sfmfromscratch_amd import distributed as D
+    from sfmfromscratch_amd import synth
+    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, SlotTable
+
+    Bx = 32
+    n_global = args.frames or (2048 if args.scaling == "strong" else 256)
+    if args.scaling == "weak":
+        n_global *= world
+    plan = D.GatherPlan(n_global, world, Bx, args.pairs)
+    S, C = plan.S, plan.C
+    halo = args.exchange == "halo"
+    if halo and args.pairs != "consecutive":
+        raise SystemExit("--exchange halo serves consecutive pairs only")
+    # this rank's frames, uint8, device-resident
+    U = min(S, 64)
+    uniq = np.stack([synth.make_frame_u8(H, W, 1234, rank * S + i) for i in range(U)])
+    uq = torch.from_numpy(uniq).to(dev)
+    del uniq
+    frames = uq[torch.arange(S, device=dev) % U].contiguous()
+    del uq
+
+    lanes = []
+    for _ in range(max(1, args.inflight)):
+        ex = BatchExtractor(P_OCT, device=dev.index)
+        ex.reserve(Bx, H, W)
+        lanes.append({"ex": ex, "stream": torch.cuda.Stream(device=dev)})
+    cap = lanes[0]["ex"].cap
+    matcher = BatchMatcher(RATIO, device=dev.index)  # own context: matches run on their own stream
+    mstream = torch.cuda.Stream(device=dev)
+
+    if halo:
+        # local table: slots [0, S) = own frames in order, slot S = rank r+1's first frame
+        table = SlotTable(torch, S + 1, cap, dev)
+        lp = D.local_consecutive_pairs(S, rank, world)
+        ready = np.minimum(lp[:, 1] // Bx, C - 1)  # pair (l, l+1) is ready with l+1's chunk
+        sched = [lp[ready == c] for c in range(C)]
+        rank_pairs_n = len(lp)
+        for ln in lanes:
+            ln["slots"] = None
+    else:
+        table = SlotTable(torch, n_global, cap, dev)
+        if args.pairs == "all":
+            sched = None
+            rank_pairs_n = None
+        else:
+            rp = plan.rank_pairs(rank)
+            sched = plan.schedule(rp)
+            rank_pairs_n = len(rp)
+        for ln in lanes:
+            ln["slots"] = SlotTable(torch, Bx, cap, dev) if world > 1 else None
+
+    def view(tab, lo, n):
+        v = SlotTable.__new__(SlotTable)
+        v.B, v.cap = n, tab.cap
+        v.xy, v.desc, v.count = tab.xy[lo:lo + n], tab.desc[lo:lo + n], tab.count[lo:lo + n]
+        return v
+
+    def new_out(P):
+        P = max(P, 1)
+        return (torch.zeros((P, cap, 2), dtype=torch.int32, device=dev),
+                torch.zeros((P, cap), dtype=torch.float32, device=dev),
+                torch.zeros((P,), dtype=torch.int32, device=dev))
+
+    CH = 4096  # 'all': pairs per matcher launch (output buffer reused)
+    if sched is not None:
+        sched_dev = [torch.from_numpy(np.ascontiguousarray(p, np.int32)).to(dev) for p in sched]
+        outs = [new_out(len(p)) for p in sched]
+    else:
+        out_all = new_out(CH)
+    all_pairs_np = plan.global_pairs() if args.pairs == "all" else None
+    comm_bytes = {"sent": 0, "gathered": 0}
+    slot_bytes = cap * (128 * 4 + 2 * 4) + 4
+
+    def step():
+        cur = torch.cuda.current_stream()
+        for ln in lanes:
+            ln["stream"].wait_stream(cur)
+            ln["pending"] = None
+        mstream.wait_stream(cur)
+        for c in range(C):
+            ln = lanes[c % len(lanes)]
+            bc = plan.chunk_size(c)
+            l0 = c * Bx
+            works = None
+            with torch.cuda.stream(ln["stream"]):
+                if ln["pending"]:  # the lane's slots are free again once their gather is done
+                    for w in ln["pending"]:
+                        w.wait()
+                if halo:
+                    ln["ex"].extract(frames[l0:l0 + bc], out=view(table, l0, bc))
+                    if c == 0 and world > 1:
+                        D.halo_exchange(dist, table, S, rank, world)
+                elif world == 1:
+                    ln["ex"].extract(frames[l0:l0 + bc], out=view(table, plan.chunk_base(c), bc))
+                else:
+                    ln["ex"].extract(frames[l0:l0 + bc], out=view(ln["slots"], 0, bc))
+                    works = D.allgather_chunk(dist, table, plan, c, ln["slots"], async_op=True)
+                    ln["pending"] = works
+            if sched is None:
+                continue
+            with torch.cuda.stream(mstream):
+                if works:
+                    for w in works:
+                        w.wait()
+                elif halo and c == C - 1:  # the halo slot arrived on chunk 0's lane
+                    for other in lanes:
+                        mstream.wait_stream(other["stream"])
+                else:
+                    mstream.wait_stream(ln["stream"])
+                # this chunk's slots get their matcher operands once; pairs of earlier
+                # chunks' slots reuse theirs
+                if halo:
+                    matcher.prep(table, l0, bc + (1 if c == C - 1 and world > 1 else 0))
+                else:
+                    matcher.prep(table, plan.chunk_base(c), world * bc)
+                if len(sched[c]):
+                    matcher.match(table, sched_dev[c], out=outs[c], prepped=True)
+        for ln in lanes:
+            cur.wait_stream(ln["stream"])
+            if ln["pending"]:
+                for w in ln["pending"]:
+                    w.wait()
+        cur.wait_stream(mstream)
+        if sched is None:  # 'all': deal by cost once the counts are gathered (host sync)
+            counts = table.count.cpu().numpy()
+            mine = D.weighted_deal(all_pairs_np, counts[plan.slot_of(np.arange(n_global))], world)[rank]
+            sp = torch.from_numpy(plan.slot_of(mine).reshape(-1, 2)).to(dev)
+            matcher.prep(table)
+            for a in range(0, len(sp), CH):
+                n = min(CH, len(sp) - a)
+                matcher.match(table, sp[a:a + n], out=(out_all[0][:n], out_all[1][:n], out_all[2][:n]),
+                              prepped=True)
+            step.pairs = len(mine)
+
+    step.pairs = rank_pairs_n
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # collectives alone (untimed): the chunked all-gather with nothing else on the GPU
+    comm = None
+    if world > 1 and not halo:
+        src = lanes[0]["slots"]
+        reps = 3
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            for c in range(C):
+                for w in D.allgather_chunk(dist, table, plan, c, src, async_op=True):
+                    w.wait()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / reps
+        sent = S * slot_bytes
+        gathered = n_global * slot_bytes
+        comm = {"kind": "all_gather_into_tensor x3 fields per chunk (RCCL)", "chunks": C,
+                "bytes_sent_per_rank": sent, "bytes_gathered_per_rank": gathered,
+                "ms_alone": round(dt * 1e3, 3), "algbw_GBps": round(gathered / dt / 1e9, 1)}
+    elif world > 1:
+        comm = {"kind": "halo: 1 slot point-to-point (RCCL send/recv)", "bytes_sent_per_rank": slot_bytes}
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = max(time.perf_counter() - t0, ev0.elapsed_time(ev1) / 1e3)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    counts = table.count.cpu().numpy()
+    nm = (torch.cat([o[2][:max(len(p), 1)] for o, p in zip(outs, sched)]).cpu().numpy()
+          if sched is not None else out_all[2].cpu().numpy())
+    pairs_total = torch.tensor([step.pairs or 0], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(pairs_total)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "images/sec detect+describe+match, 1080p, 1/2/4/8 MI355X",
+            "value": round(n_global * args.steps / elapsed, 2), "unit": "images/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (deterministic integer-generated textured 1080p frames, device-resident uint8, "
+                    f"{U} distinct per rank, tiled)",
+            "config": {"workload": f"BASELINE configs[3]: {n_global}x 1080p sharded {S} per GPU, ScaleRotInvSIFT "
+                                   "4-level x2 octave pyramid, k=2500, NNRatio 0.85, "
+                                   + ("1-slot halo exchange" if halo else "chunked RCCL all-gather of the "
+                                      "descriptor tables") + f", {args.pairs} pairs",
+                       "frames_global": n_global, "frames_per_gpu": S, "chunk": Bx, "chunks": C,
+                       "pairs_global": int(pairs_total.item()), "pair_schedule": args.pairs,
+                       "exchange": args.exchange, "keypoints_mean": float(counts.mean()),
+                       "matches_mean_rank0": float(nm[nm >= 0].mean()) if (nm >= 0).any() else 0.0,
+                       "parallelism": f"image-shard x{world}", "batches_in_flight": args.inflight},
+            "collective": comm,
+            "roofline": None,
+            "cpu_baseline": None}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

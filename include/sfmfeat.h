@@ -214,6 +214,24 @@ int32_t sfm_match_pairs_dev(sfm_ctx* ctx, const float* desc, const int32_t* coun
                             int64_t cap, const int32_t* pairs, int32_t P, float ratio,
                             int32_t* matches, float* conf, int32_t* nmatch, void* stream);
 
+/*
+ * The same matcher split in two for large resident tables (BASELINE configs[3]'s gathered
+ * table of thousands of slots, matched a chunk of pairs at a time):
+ *  - sfm_match_prep_dev builds the matcher's per-descriptor operands (split-f16 copies,
+ *    norms, per-slot maxima) for slots [slot_lo, slot_lo + slot_n) of a table of `nimg`
+ *    slots into ctx-owned buffers sized for the whole table;
+ *  - sfm_match_pairs_prepped_dev matches pairs whose slots were all prepped by earlier
+ *    calls on this ctx (same table, descriptors unchanged since) — sfm_match_pairs_dev
+ *    without its prep of every slot.
+ * Results are identical to sfm_match_pairs_dev.  Same pairs / outputs / status rules.
+ */
+int32_t sfm_match_prep_dev(sfm_ctx* ctx, const float* desc, const int32_t* count, int32_t nimg,
+                           int64_t cap, int32_t slot_lo, int32_t slot_n, void* stream);
+int32_t sfm_match_pairs_prepped_dev(sfm_ctx* ctx, const float* desc, const int32_t* count,
+                                    int32_t nimg, int64_t cap, const int32_t* pairs, int32_t P,
+                                    float ratio, int32_t* matches, float* conf, int32_t* nmatch,
+                                    void* stream);
+
 /* ---------------- stage profiling (bench.py's live roofline numbers) ----------------
  * When enabled, every stage's launches are bracketed by HIP events on the launch
  * stream; sfm_profile_read synchronises them and returns the accumulated device time

@@ -57,6 +57,10 @@ SIGNATURES = {
                                                   _vp, _vp, ctypes.c_int64, _vp]),
     "sfm_match_pairs_dev": (ctypes.c_int32, [_vp, _vp, _vp, ctypes.c_int32, ctypes.c_int64, _vp, ctypes.c_int32,
                                              ctypes.c_float, _vp, _vp, _vp, _vp]),
+    "sfm_match_prep_dev": (ctypes.c_int32, [_vp, _vp, _vp, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
+                                            ctypes.c_int32, _vp]),
+    "sfm_match_pairs_prepped_dev": (ctypes.c_int32, [_vp, _vp, _vp, ctypes.c_int32, ctypes.c_int64, _vp,
+                                                     ctypes.c_int32, ctypes.c_float, _vp, _vp, _vp, _vp]),
     "sfm_profile_enable": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "sfm_profile_stages": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "sfm_profile_read": (ctypes.c_int32, [_vp, ctypes.POINTER(ctypes.c_double), _i64p, ctypes.c_int32]),
@@ -283,10 +287,16 @@ class Context:
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.PROF_STAGES)}
 
     def match_pairs_dev(self, desc_ptr: int, count_ptr: int, nimg: int, cap: int, pairs_ptr: int, P: int,
-                        ratio32: float, matches_ptr: int, conf_ptr: int, nmatch_ptr: int, stream: int = 0):
-        check(self.lib.sfm_match_pairs_dev(self.handle, desc_ptr, count_ptr, nimg, cap, pairs_ptr, P,
-                                           ctypes.c_float(ratio32), matches_ptr, conf_ptr, nmatch_ptr,
-                                           stream or None), self.handle)
+                        ratio32: float, matches_ptr: int, conf_ptr: int, nmatch_ptr: int, stream: int = 0,
+                        prepped: bool = False):
+        fn = self.lib.sfm_match_pairs_prepped_dev if prepped else self.lib.sfm_match_pairs_dev
+        check(fn(self.handle, desc_ptr, count_ptr, nimg, cap, pairs_ptr, P, ctypes.c_float(ratio32), matches_ptr,
+                 conf_ptr, nmatch_ptr, stream or None), self.handle)
+
+    def match_prep_dev(self, desc_ptr: int, count_ptr: int, nimg: int, cap: int, slot_lo: int, slot_n: int,
+                       stream: int = 0):
+        check(self.lib.sfm_match_prep_dev(self.handle, desc_ptr, count_ptr, nimg, cap, slot_lo, slot_n,
+                                          stream or None), self.handle)
 
 
 def debug_atan2(y: np.ndarray, x: np.ndarray, device: int = 0) -> np.ndarray:

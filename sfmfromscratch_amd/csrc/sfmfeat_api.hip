@@ -368,45 +368,65 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   return SFM_OK;
 }
 
-int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, int64_t cap,
-               const int32_t* pairs, int P, float ratio, int32_t* matches, float* conf,
-               int32_t* nmatch, hipStream_t st) {
-  if (P <= 0) return SFM_OK;
+// Matcher operands for slots [lo, lo + n) of a table of nimg slots (buffers sized for
+// the whole table; the kernels index slots relative to the offset base pointers).
+int match_prep_range(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, int64_t cap, int lo, int n,
+                     hipStream_t st) {
   if (cap < 1 || cap > kMaxMatchRows)
     return set_err(c, SFM_EINVAL, "match capacity must be in [1, 16384]");
+  if (lo < 0 || n < 0 || lo + n > nimg) return set_err(c, SFM_EINVAL, "prep slot range outside the table");
   int rc;
+  const float* d0 = desc + (int64_t)lo * cap * 128;
   if (c->match_direct) {
-    int64_t capP = (cap + 63) / 64 * 64;
+    const int64_t capP = (cap + 63) / 64 * 64;
     if ((rc = ensure(c, c->m_descT, (size_t)nimg * 128 * capP * 4))) return rc;
-    if ((rc = ensure(c, c->m_rows, (size_t)P * cap * sizeof(RowBest)))) return rc;
-    {
-      StageScope sc(c, SFM_PROF_MATCH_PREP, st);
-      launch_transpose_desc(desc, count, nimg, cap, capP, as<float>(c->m_descT), st);
-    }
-    {
-      StageScope sc(c, SFM_PROF_MATCH, st);
-      launch_match_rows(as<float>(c->m_descT), count, capP, pairs, P, ratio, as<RowBest>(c->m_rows),
-                        (int)cap, st);
-    }
+    if (n == 0) return SFM_OK;
+    StageScope sc(c, SFM_PROF_MATCH_PREP, st);
+    launch_transpose_desc(d0, count + lo, n, cap, capP, as<float>(c->m_descT) + (int64_t)lo * 128 * capP, st);
   } else {
-    int64_t capP = (cap + 127) / 128 * 128;
+    const int64_t capP = (cap + 127) / 128 * 128;
     if ((rc = ensure(c, c->m_hi, (size_t)nimg * capP * 128 * 2))) return rc;
     if ((rc = ensure(c, c->m_lo, (size_t)nimg * capP * 128 * 2))) return rc;
     if ((rc = ensure(c, c->m_norm2, (size_t)nimg * capP * 4))) return rc;
     if ((rc = ensure(c, c->m_rnorm, (size_t)nimg * capP * 4))) return rc;
     if ((rc = ensure(c, c->m_imgmax, (size_t)nimg * 8))) return rc;
-    if ((rc = ensure(c, c->m_rows, (size_t)P * cap * sizeof(RowBest)))) return rc;
-    {
-      StageScope sc(c, SFM_PROF_MATCH_PREP, st);
-      launch_match_prep(desc, count, nimg, cap, capP, as<_Float16>(c->m_hi), as<_Float16>(c->m_lo),
-                        as<float>(c->m_norm2), as<float>(c->m_rnorm), as<unsigned int>(c->m_imgmax), st);
-    }
-    {
-      StageScope sc(c, SFM_PROF_MATCH, st);
-      launch_match_mfma(desc, count, cap, capP, as<_Float16>(c->m_hi), as<_Float16>(c->m_lo),
-                        as<float>(c->m_norm2), as<float>(c->m_rnorm), as<unsigned int>(c->m_imgmax), pairs,
-                        P, ratio, as<RowBest>(c->m_rows), (int)cap, st);
-    }
+    if (n == 0) return SFM_OK;
+    StageScope sc(c, SFM_PROF_MATCH_PREP, st);
+    const int64_t o = (int64_t)lo * capP;
+    launch_match_prep(d0, count + lo, n, cap, capP, as<_Float16>(c->m_hi) + o * 128, as<_Float16>(c->m_lo) + o * 128,
+                      as<float>(c->m_norm2) + o, as<float>(c->m_rnorm) + o, as<unsigned int>(c->m_imgmax) + 2 * lo,
+                      st);
+  }
+  HIPCHK(c, hipGetLastError());
+  return SFM_OK;
+}
+
+int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, int64_t cap,
+               const int32_t* pairs, int P, float ratio, int32_t* matches, float* conf,
+               int32_t* nmatch, hipStream_t st, bool prep = true) {
+  if (P <= 0) return SFM_OK;
+  if (cap < 1 || cap > kMaxMatchRows)
+    return set_err(c, SFM_EINVAL, "match capacity must be in [1, 16384]");
+  int rc;
+  if (prep) {
+    if ((rc = match_prep_range(c, desc, count, nimg, cap, 0, nimg, st))) return rc;
+  } else {  // operands from earlier sfm_match_prep_dev calls: the buffers must cover the table
+    const int64_t capP = c->match_direct ? (cap + 63) / 64 * 64 : (cap + 127) / 128 * 128;
+    const size_t need = c->match_direct ? (size_t)nimg * 128 * capP * 4 : (size_t)nimg * capP * 128 * 2;
+    if ((c->match_direct ? c->m_descT.bytes : c->m_hi.bytes) < need)
+      return set_err(c, SFM_ESTATE, "sfm_match_pairs_prepped_dev before sfm_match_prep_dev for this table");
+  }
+  if ((rc = ensure(c, c->m_rows, (size_t)P * cap * sizeof(RowBest)))) return rc;
+  if (c->match_direct) {
+    const int64_t capP = (cap + 63) / 64 * 64;
+    StageScope sc(c, SFM_PROF_MATCH, st);
+    launch_match_rows(as<float>(c->m_descT), count, capP, pairs, P, ratio, as<RowBest>(c->m_rows), (int)cap, st);
+  } else {
+    const int64_t capP = (cap + 127) / 128 * 128;
+    StageScope sc(c, SFM_PROF_MATCH, st);
+    launch_match_mfma(desc, count, cap, capP, as<_Float16>(c->m_hi), as<_Float16>(c->m_lo), as<float>(c->m_norm2),
+                      as<float>(c->m_rnorm), as<unsigned int>(c->m_imgmax), pairs, P, ratio, as<RowBest>(c->m_rows),
+                      (int)cap, st);
   }
   {
     StageScope sc(c, SFM_PROF_MATCH_POST, st);
@@ -732,9 +752,9 @@ int ransac_impl(sfm_ctx* c, const int32_t* pts, const int32_t* npts_dev, const i
   if ((rc = ensure(c, c->r_counts, (size_t)P * std::max(iters, 1) * 4))) return rc;
   HIPCHK(c, hipMemcpyAsync(c->r_idx.p, all.data(), all.size() * 4, hipMemcpyHostToDevice, st));
   HIPCHK(c, hipMemcpyAsync(c->r_off.p, off.data(), (size_t)P * 4, hipMemcpyHostToDevice, st));
-  if (iters > 0)
-    launch_ransac(pts, npts_dev, nmax, P, as<int32_t>(c->r_idx), as<int32_t>(c->r_off), iters, thr, as<double>(c->r_F),
-                  as<int32_t>(c->r_counts), out_pts, out_n, out_iter, st);
+  // iters == 0 still launches the select kernel: it writes every pair's empty / None result
+  launch_ransac(pts, npts_dev, nmax, P, as<int32_t>(c->r_idx), as<int32_t>(c->r_off), iters, thr, as<double>(c->r_F),
+                as<int32_t>(c->r_counts), out_pts, out_n, out_iter, st);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(st));  // the host index buffers above are stack-owned
   return SFM_OK;
@@ -942,6 +962,23 @@ int32_t sfm_match_pairs_dev(sfm_ctx* c, const float* desc, const int32_t* count,
   HIPCHK(c, hipSetDevice(c->device));
   hipStream_t st = (hipStream_t)stream;  // exactly the caller's stream (NULL = null stream)
   return match_impl(c, desc, count, nimg, cap, pairs, P, ratio, matches, conf, nmatch, st);
+}
+
+int32_t sfm_match_prep_dev(sfm_ctx* c, const float* desc, const int32_t* count, int32_t nimg, int64_t cap,
+                           int32_t slot_lo, int32_t slot_n, void* stream) {
+  if (!c || !desc || !count || nimg < 1) return SFM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  return match_prep_range(c, desc, count, nimg, cap, slot_lo, slot_n, (hipStream_t)stream);
+}
+
+int32_t sfm_match_pairs_prepped_dev(sfm_ctx* c, const float* desc, const int32_t* count, int32_t nimg,
+                                    int64_t cap, const int32_t* pairs, int32_t P, float ratio, int32_t* matches,
+                                    float* conf, int32_t* nmatch, void* stream) {
+  if (!c || !desc || !count || !pairs || !matches || !conf || !nmatch || nimg < 1 || P < 0)
+    return SFM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  return match_impl(c, desc, count, nimg, cap, pairs, P, ratio, matches, conf, nmatch, (hipStream_t)stream,
+                    false);
 }
 
 }  // extern "C"

@@ -94,9 +94,21 @@ class BatchMatcher:
         self.ctx = ctx or Context(_abi.params_from_dict({}, _abi.SFM_MODE_NAIVE), device)
         self.device = device
 
-    def match(self, slots: SlotTable, pairs, out=None):
+    def prep(self, slots: SlotTable, lo: int = 0, n: int | None = None):
+        """Build the matcher's operands for slots [lo, lo + n) of `slots` (default: all) on
+        torch's current stream; later `match(..., prepped=True)` calls on pairs of prepped
+        slots skip the per-call prep of the whole table (large resident tables)."""
+        torch = self.torch
+        S, cap = slots.desc.shape[0], slots.desc.shape[1]
+        n = S - lo if n is None else n
+        stream = torch.cuda.current_stream(slots.desc.device).cuda_stream
+        self.ctx.match_prep_dev(slots.desc.data_ptr(), slots.count.data_ptr(), S, cap, lo, n, stream)
+
+    def match(self, slots: SlotTable, pairs, out=None, prepped: bool = False):
         """pairs: (P, 2) int32 tensor on the device.  Returns (matches [P,cap,2] int32,
-        conf [P,cap] f32, nmatch [P] int32 (-1 = the reference's IndexError))."""
+        conf [P,cap] f32, nmatch [P] int32 (-1 = the reference's IndexError)).  With
+        `prepped`, every slot the pairs touch must have been prepped by `prep` since its
+        descriptors last changed."""
         torch = self.torch
         P = int(pairs.shape[0])
         cap = slots.desc.shape[1]
@@ -110,7 +122,7 @@ class BatchMatcher:
         stream = torch.cuda.current_stream(dev).cuda_stream
         self.ctx.match_pairs_dev(slots.desc.data_ptr(), slots.count.data_ptr(), slots.desc.shape[0], cap,
                                  pairs.data_ptr(), P, self.ratio32, out[0].data_ptr(), out[1].data_ptr(),
-                                 out[2].data_ptr(), stream)
+                                 out[2].data_ptr(), stream, prepped=prepped)
         return out
 
 

@@ -55,6 +55,37 @@ def _worker(rank, world, port, n_global, mode, errq):
             else:
                 assert int(slots.count[n_local]) == 0  # untouched
             glob = [(lo + int(i), lo + int(j)) for i, j in pairs]
+        elif mode.startswith("plan"):  # configs[3]: chunked all-gather (distributed.GatherPlan)
+            sched_name = mode.split("/", 1)[1]
+            plan = D.GatherPlan(n_global, world, 3, sched_name)
+            table = SlotTable(torch, n_global, CAP, "cpu")
+            src = SlotTable(torch, plan.chunk, CAP, "cpu")
+            for c in range(plan.C):
+                lo, hi = plan.local_frames(rank, c)
+                for b, g in enumerate(range(lo, hi)):
+                    _fill_slot(src, b, g)
+                for w in D.allgather_chunk(dist, table, plan, c, src, async_op=True):
+                    w.wait()
+            for g in range(n_global):  # every frame at slot_of(g), bit-equal
+                ref = SlotTable(torch, 1, CAP, "cpu")
+                _fill_slot(ref, 0, g)
+                s = int(plan.slot_of(g))
+                assert torch.equal(table.desc[s], ref.desc[0]) and torch.equal(table.xy[s], ref.xy[0])
+                assert int(table.count[s]) == int(ref.count[0])
+            assert sorted(plan.frame_of_slot().tolist()) == list(range(n_global))
+            if sched_name == "all":
+                counts = table.count.numpy()[plan.slot_of(np.arange(n_global))]
+                mine = D.weighted_deal(plan.global_pairs(), counts, world)[rank]
+            else:
+                mine = plan.rank_pairs(rank)
+            glob = []
+            inv = plan.frame_of_slot()
+            for c, sp in enumerate(plan.schedule(mine)):
+                for a, b in sp.tolist():
+                    i, j = int(inv[a]), int(inv[b])
+                    # ready: both frames' chunks gathered by chunk c
+                    assert plan.chunk_of(i) <= c and plan.chunk_of(j) <= c
+                    glob.append((i, j))
         else:  # allgather
             per = -(-n_global // world)
             slots = SlotTable(torch, per, CAP, "cpu")
@@ -73,8 +104,11 @@ def _worker(rank, world, port, n_global, mode, errq):
         dist.all_gather_object(gathered, glob)
         if rank == 0:
             allp = sorted(p for g in gathered for p in g)
-            if mode == "halo":
+            if mode in ("halo", "plan/consecutive"):
                 expect = [(i, i + 1) for i in range(n_global - 1)]
+            elif mode.startswith("plan/window:"):
+                w = int(mode.split(":")[1])
+                expect = sorted((i, i + d) for d in range(1, w + 1) for i in range(n_global - d))
             else:
                 expect = [(i, j) for i in range(n_global) for j in range(i + 1, n_global)]
             assert allp == expect, (allp, expect)
@@ -112,6 +146,34 @@ def test_halo_exchange_consecutive_pairs(world, n_global):
 @pytest.mark.parametrize("world,n_global", [(2, 6), (3, 7)])
 def test_allgather_all_pairs(world, n_global):
     _run(world, n_global, "allgather")
+
+
+@pytest.mark.parametrize("world,n_global,sched", [(2, 16, "consecutive"), (2, 14, "window:4"), (3, 21, "all"),
+                                                  (3, 9, "consecutive")])
+def test_chunked_allgather_plan(world, n_global, sched):
+    """configs[3]'s schedule: chunked all-gather lands every frame bit-equal at its table
+    slot on every rank; the ranks' pairs cover the global schedule exactly once, each in a
+    chunk at which both of its frames are gathered."""
+    _run(world, n_global, "plan/" + sched)
+
+
+def test_gather_plan_layout_and_weighted_deal():
+    plan = D.GatherPlan(64, 4, 5)  # S = 16 per rank: chunks of 5, 5, 5, 1
+    assert plan.C == 4 and [plan.chunk_size(c) for c in range(4)] == [5, 5, 5, 1]
+    slots = plan.slot_of(np.arange(64))
+    assert sorted(slots.tolist()) == list(range(64))
+    for c in range(plan.C):  # one chunk's region is contiguous and rank-major
+        region = [int(plan.slot_of(g)) for r in range(4) for g in range(*plan.local_frames(r, c))]
+        assert region == list(range(plan.chunk_base(c), plan.chunk_base(c) + 4 * plan.chunk_size(c)))
+    with pytest.raises(ValueError):
+        D.GatherPlan(10, 4, 2)
+    with pytest.raises(ValueError):
+        D.GatherPlan(8, 2, 2, "bogus")
+    counts = np.array([10, 1, 1, 1, 10, 1], np.int64)
+    deal = D.weighted_deal(D.all_pairs(6), counts, 2)
+    cost = [sum(int(counts[i] * counts[j] + 1) for i, j in d) for d in deal]
+    assert sum(len(d) for d in deal) == 15 and abs(cost[0] - cost[1]) <= 101
+    assert {tuple(p) for d in deal for p in d.tolist()} == {tuple(p) for p in D.all_pairs(6).tolist()}
 
 
 def test_shard_range_partitions():

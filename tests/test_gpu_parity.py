@@ -348,3 +348,58 @@ def test_all_pairs_schedule_vs_oracle():
         om, oc = O.match(desc[i, :counts[i]], desc[j, :counts[j]], 0.85)
         k = int(nm[p])
         assert_matches_equal(om, oc, mm[p, :k].cpu().numpy(), mc[p, :k].cpu().numpy())
+
+
+def test_configs2_workload_1080p_all_pairs_vs_oracle():
+    """BASELINE configs[2] at its own frame size and parameters: 10 x 1080p frames, the
+    4-level octave pyramid with k = 2500, every one of the 45 pairs matched.  Keypoints and
+    descriptors bit-equal to the oracle's, every pair's matches equal to the oracle's
+    matcher on those descriptors (the C oracle runs on host threads)."""
+    torch = pytest.importorskip("torch")
+    from concurrent.futures import ThreadPoolExecutor
+
+    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, all_pairs
+    B, H, W = 10, 1080, 1920
+    u8 = synth.make_batch_u8(B, H, W, seed=1234)
+    ex = BatchExtractor(P_OCT)
+    s = ex.extract(torch.from_numpy(synth.u8_to_gray(u8)).cuda())
+    pairs_np = all_pairs(B)
+    mm, mc, nm = BatchMatcher(0.85, ctx=ex.ctx).match(s, torch.from_numpy(pairs_np).cuda())
+    torch.cuda.synchronize()
+    counts, xy, desc = s.count.cpu().numpy(), s.xy.cpu().numpy(), s.desc.cpu().numpy()
+    mm, mc, nm = mm.cpu().numpy(), mc.cpu().numpy(), nm.cpu().numpy()
+    gray = synth.u8_to_gray(u8)
+    with ThreadPoolExecutor(16) as pool:
+        ext = list(pool.map(lambda i: O.extract(gray[i], P_OCT), range(B)))
+        for i, (OX, OY, OD, _) in enumerate(ext):
+            n = int(counts[i])
+            assert n == len(OX) and n > 1500
+            assert np.array_equal(xy[i, :n, 0], OX) and np.array_equal(xy[i, :n, 1], OY)
+            assert np.array_equal(bits(desc[i, :n]), bits(OD))
+        om = list(pool.map(lambda p: O.match(desc[p[0], :counts[p[0]]], desc[p[1], :counts[p[1]]], 0.85),
+                           [tuple(p) for p in pairs_np]))
+    for p in range(len(pairs_np)):
+        k = int(nm[p])
+        assert_matches_equal(om[p][0], om[p][1], mm[p, :k], mc[p, :k])
+
+
+def test_prep_ranges_then_prepped_match_equal_full_match():
+    """sfm_match_prep_dev over slot ranges + sfm_match_pairs_prepped_dev (the configs[3]
+    chunked path) give exactly sfm_match_pairs_dev's results; prepped matching on a fresh
+    context is refused (SFM_ESTATE -> RuntimeError)."""
+    torch = pytest.importorskip("torch")
+    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, all_pairs
+    B, H, W = 6, 270, 480
+    ex = BatchExtractor(dict(P_OCT, num_interest_points=800))
+    s = ex.extract(torch.from_numpy(synth.make_batch_u8(B, H, W, seed=93)).cuda())
+    pairs = torch.from_numpy(all_pairs(B)).cuda()
+    ref = BatchMatcher(0.85).match(s, pairs)
+    m = BatchMatcher(0.85)
+    with pytest.raises(RuntimeError):
+        m.match(s, pairs, prepped=True)
+    m.prep(s, 0, 2)
+    m.prep(s, 2, 4)
+    got = m.match(s, pairs, prepped=True)
+    torch.cuda.synchronize()
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
