@@ -220,6 +220,6 @@ void launch_match_prep(const float* desc, const int32_t* count, int nimg, int64_
 void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int64_t capP,
                        const _Float16* hi, const _Float16* lo, const float* norm2, const float* rnorm,
                        const unsigned int* imgmax, const int32_t* pairs, int P, float ratio,
-                       RowBest* rows, int max_rows, hipStream_t st);
+                       RowBest* rows, int max_rows, int* ovf_count, int2* ovf_list, hipStream_t st);
 
 }  // namespace sfm

@@ -6,17 +6,18 @@
 //   1. approximate d^2 = |a|^2 + |b|^2 - 2 a.b for every target with fp16 split operands
 //      (a = hi + lo * 2^-11, three f16 MFMA products hi.hi + (hi.lo + lo.hi), f32
 //      accumulation, operands pre-scaled by 2^8 to keep them out of the f16 subnormal
-//      range), tracking each row's running second-smallest approximate value D2~;
-//   2. in the same sweep collect every target with d~ <= D2~(so far) + 2 E_i, where E_i
-//      bounds |d~ - d_ref| rigorously (fp16 representation, dropped lo.lo term, f32
-//      accumulation error <= K u sum|ab|, f32 rounding of d~ and of the reference's own
-//      pairwise sum); D2~(so far) >= the final D2~, so the collection contains the final
-//      window, and any target outside it is strictly farther than the second nearest;
-//   3. recompute the collected candidates with the reference's exact float32 pairwise
-//      order (8 accumulators) and take (distance, index) minima -> ratio test.
-// Rows whose window overflows the per-row candidate list are recomputed exactly over
-// all targets (rare: only for runs of near-identical target descriptors).
+//      range), tracking each row's second-smallest approximate value D2~ (sweep 1);
+//   2. a second sweep collects every target with d~ <= D2~ + 2 E_i, where E_i bounds
+//      |d~ - d_ref| rigorously (fp16 representation, dropped lo.lo term, f32 accumulation
+//      error <= K u sum|ab|, f32 rounding of d~ and of the reference's own pairwise sum):
+//      any target outside that window is strictly farther than the second nearest;
+//   3. recompute the window with the reference's exact float32 pairwise order (8
+//      accumulators) and take (distance, index) minima -> ratio test.
+// Rows whose window overflows the per-row LDS list (runs of near-identical target
+// descriptors) are recomputed exactly over all targets by k_match_overflow.
 #include <stdlib.h>
+
+#include <type_traits>
 
 #include "kernels.h"
 
@@ -29,7 +30,7 @@ constexpr int kQW = 32;                // query rows per wave
 constexpr int kWaves = 4;              // waves per workgroup
 constexpr int kQB = kQW * kWaves;      // 128 query rows per workgroup
 constexpr int kRowH = 128 + 8;         // padded fp16 row in LDS (272 B): conflict-free b128 reads
-constexpr int kCandCap = 64;           // exact re-rank candidates per query row
+constexpr int kCandCap = 128;          // window members per query row kept in LDS
 constexpr float kScale = 256.0f;       // operand pre-scale (2^8)
 constexpr float kLoScale = 2048.0f;    // lo part scale (2^11)
 
@@ -125,12 +126,6 @@ SFM_DEV float exact_sqdist(const float* __restrict__ a, const float* __restrict_
   return u0 + u1;
 }
 
-// d~ rounded DOWN to bf16 (kept as its top 16 bits): truncation for positive values;
-// negative values (|d~| within E of 0) become -inf, which always passes the filter
-SFM_DEV uint16_t bf16_down(float v) {
-  return v >= 0.0f ? (uint16_t)(__float_as_uint(v) >> 16) : (uint16_t)0xFF80u;
-}
-
 SFM_DEV void top2_merge(float& b1, int& j1, float& b2, float ob1, int oj1, float ob2) {
   if (ob1 < b1 || (ob1 == b1 && oj1 < j1)) {
     b2 = fminf(b1, ob2);
@@ -143,33 +138,39 @@ SFM_DEV void top2_merge(float& b1, int& j1, float& b2, float ob1, int oj1, float
 
 constexpr int kTT2 = 64;               // targets per LDS stage (two 32-target MFMA sub-tiles)
 constexpr int kStageHalves = kTT2 * kRowH;  // f16 elements per array per stage
-static_assert(kCandCap <= 64, "admission masks are 64-bit at most");
+constexpr int kScr = 2 * kStageHalves / 2;  // re-rank scratch floats in the stage buffers (8704)
 
-// One workgroup = 4 waves x 32 query rows.  Single sweep over the targets in 64-row stages:
-// the next stage's hi/lo rows are loaded into registers while the current stage's MFMAs
-// run, then stored into the (single) LDS stage buffer.  Per lane the running top-2 of the approximate distances
-// gives a threshold thr = b2~ + 2E that only shrinks, so every target inside the final
-// window (d~ <= b2~_final + 2E) is admitted when visited; the admitted targets are then
-// re-ranked with the reference's exact float32 distance.
-// ABL (timing builds only; results are wrong unless 0): 6 = no re-rank, 8 = no appends
+// One workgroup = 4 waves x 32 query rows; two sweeps over the target table of the pair, in
+// 64-row LDS stages (the next stage's hi/lo rows are loaded into registers while the
+// current stage's MFMAs run, then stored into the single LDS stage buffer):
+//   sweep 1: the running top-2 of d~ per row (two v_med3 per element) -> the row's FINAL
+//            window thr = b2~ + 2E (both halves of the wave merged);
+//   sweep 2: the same MFMAs; every target with d~ <= thr is appended to the row's LDS list
+//            (index only: the window is exact, so no approximate distance is kept and no
+//            post-filter runs; a ballot skips the append code for stages where no lane of
+//            the wave admits anything).
+// Every target inside the window is re-ranked with the reference's exact float32 distance
+// (flattened over the workgroup, in chunks through the stage buffers).  A row whose window
+// holds more than kCandCap targets is handed to k_match_overflow (global list).
+// The window argument: the targets achieving b1~ and b2~ have exact distances <= b1~ + E and
+// <= b2~ + E, so the exact second-smallest D2 <= b2~ + E; a target with exact d <= D2 has
+// d~ <= d + E <= b2~ + 2E.  Targets outside the window are strictly farther than D2.
+// ABL (timing builds only; results are wrong unless 0): 6 = no re-rank, 8 = no sweep 2
 template <int ABL>
-__global__ void __launch_bounds__(256) k_match_mfma(
+__global__ void __launch_bounds__(256, 2) k_match_mfma(
     const float* __restrict__ desc, const int32_t* __restrict__ count, int64_t cap, int64_t capP,
     const _Float16* __restrict__ hi, const _Float16* __restrict__ lo, const float* __restrict__ norm2,
     const float* __restrict__ rnorm, const unsigned int* __restrict__ imgmax,
-    const int32_t* __restrict__ pairs, int P, float ratio, RowBest* __restrict__ rows_out, int max_rows) {
-  // stage buffer [hi|lo][64][kRowH]; after the sweep the space holds the re-rank scratch
+    const int32_t* __restrict__ pairs, int P, float ratio, RowBest* __restrict__ rows_out, int max_rows,
+    int* __restrict__ ovf_count, int2* __restrict__ ovf_list) {
+  // stage buffer [hi|lo][64][kRowH]; after the sweeps the space holds the re-rank scratch
   __shared__ __attribute__((aligned(16))) _Float16 sT[2][kStageHalves];
   __shared__ __attribute__((aligned(16))) float sN[kTT2];
   __shared__ uint16_t sCand[kQB][kCandCap];
-  __shared__ uint16_t sCandD[kQB][kCandCap];  // d~ rounded down to bf16 (for the final filter)
   __shared__ int sCnt[kQB];
   __shared__ int sOff[kQB + 1];
-  __shared__ float sThr[kQB];
-  float* sDex = reinterpret_cast<float*>(&sT[0][0]);            // [kQB][kCandCap]
-  float* sRed = sDex;                                            // [2][256] (after the re-rank)
-  int* sRedJ = reinterpret_cast<int*>(sRed + 2 * 256);           // [256]
-  static_assert(sizeof(sT) >= (size_t)kQB * kCandCap * 4, "re-rank scratch fits");
+  float* sDex = reinterpret_cast<float*>(&sT[0][0]);
+  static_assert(sizeof(sT) >= (size_t)kScr * 4, "re-rank scratch fits");
 
   // XCD-aware mapping (workgroups b and b + 8 share an XCD and its L2): group g = b % 8
   // takes the pairs p = g (mod 8), so all query blocks of a pair stream its target table
@@ -223,118 +224,105 @@ __global__ void __launch_bounds__(256) k_match_mfma(
       *reinterpret_cast<h8*>(&sT[1][lr * kRowH + lc + 8 * q]) = g[4 + q];
     }
   };
-  load_stage(0);
-  const float nrm_t0 = (tid < kTT2) ? norm2[(int64_t)i2 * capP + tid] : 0.0f;
-  store_stage();
-  if (tid < kTT2) sN[tid] = nrm_t0;
 
-  float b1 = INFINITY, b2 = INFINITY;
-  uint32_t admit_x = 0;  // ABL 8 only
-  for (int st = 0; st < nst; ++st) {
-    __syncthreads();  // stage st visible
-    float nrm_next = 0.0f;
-    if (st + 1 < nst) {
-      load_stage(st + 1);
-      if (tid < kTT2) nrm_next = norm2[(int64_t)i2 * capP + (st + 1) * kTT2 + tid];
-    }
-    const _Float16* tH = &sT[0][0];
-    const _Float16* tL = &sT[1][0];
-    float d[2][16];
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      // 32 targets x 32 queries: hi.hi into ahh, hi.lo + lo.hi into ax (one chain each)
-      f32x16 ahh = {}, ax = {};
-      const int trow = (32 * sub + (lane & 31)) * kRowH;
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const int ko = kk * 16 + 8 * half;
-        const h8 thi = *reinterpret_cast<const h8*>(tH + trow + ko);
-        const h8 tlo = *reinterpret_cast<const h8*>(tL + trow + ko);
-        ahh = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qhi[kk], ahh, 0, 0, 0);
-        ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qlo[kk], ax, 0, 0, 0);
-        ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(tlo, qhi[kk], ax, 0, 0, 0);
+  float b1 = INFINITY, b2 = INFINITY, thr = INFINITY;
+  const bool live = qi < n1;
+  // one sweep over the pair's targets; PH 0 tracks the running top-2, PH 1 appends the
+  // final window
+  auto sweep = [&](auto phc) {
+    constexpr int PH = decltype(phc)::value;
+    load_stage(0);
+    const float nrm_t0 = (tid < kTT2) ? norm2[(int64_t)i2 * capP + tid] : 0.0f;
+    store_stage();
+    if (tid < kTT2) sN[tid] = nrm_t0;
+    for (int st = 0; st < nst; ++st) {
+      __syncthreads();  // stage st visible
+      float nrm_next = 0.0f;
+      if (st + 1 < nst) {
+        load_stage(st + 1);
+        if (tid < kTT2) nrm_next = norm2[(int64_t)i2 * capP + (st + 1) * kTT2 + tid];
       }
-      // d~ = na + nb - 2 a.b with a.b = (ahh + ax 2^-11) 2^-16: two fmas by exact powers
-      // of two (each rounding is covered by E's 4e-6 (na + nb) term)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const float4 nb4 = *reinterpret_cast<const float4*>(&sN[32 * sub + 8 * g4 + 4 * half]);
-        const float nbv[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int rr = 4 * g4 + e;
-          const float t2 = na + nbv[e];
-          d[sub][rr] = __builtin_fmaf(ax[rr], -1.4901161193847656e-08f /* -2^-26 */,
-                                 __builtin_fmaf(ahh[rr], -3.0517578125e-05f /* -2^-15 */, t2));
-        }
-      }
-      // (targets past n2 are padding rows with norm2 = +inf: d = +inf)
-      // running top-2 (b1 <= b2): b2 = med3(b1, b2, d), b1 = med3(b1, d, -inf) = min
-#pragma unroll
-      for (int rr = 0; rr < 16; ++rr) {
-        b2 = __builtin_amdgcn_fmed3f(b1, b2, d[sub][rr]);
-        b1 = __builtin_amdgcn_fmed3f(b1, d[sub][rr], -INFINITY);
-      }
-    }
-    // once per stage (a branch inside the sub-tile loop would split the block and stop the
-    // compiler overlapping one sub-tile's MFMAs with the other's epilogue): the row's
-    // running threshold (both halves merged; b2 only decreases, so it stays conservative),
-    // then the appends
-    {
-      const float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
-      const float thr = fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + 2.0f * E;
+      const _Float16* tH = &sT[0][0];
+      const _Float16* tL = &sT[1][0];
       uint32_t mm = 0;
 #pragma unroll
-      for (int sub = 0; sub < 2; ++sub)
+      for (int sub = 0; sub < 2; ++sub) {
+        // 32 targets x 32 queries: hi.hi into ahh, hi.lo + lo.hi into ax (one chain each)
+        f32x16 ahh = {}, ax = {};
+        const int trow = (32 * sub + (lane & 31)) * kRowH;
 #pragma unroll
-        for (int rr = 0; rr < 16; ++rr) mm |= (d[sub][rr] <= thr) ? (1u << (16 * sub + rr)) : 0u;
-      if (ABL == 8) {
-        admit_x ^= mm;
-      } else if (qi < n1 && mm) {  // reserve this lane's slots with one LDS atomic, then fill them
-        int slot = atomicAdd(&sCnt[ql], __popc(mm));
-        for (; mm; mm &= mm - 1, ++slot) {
-          const int bit = __builtin_ctz(mm), rr = bit & 15;
-          const int j = st * kTT2 + 32 * (bit >> 4) + 4 * half + (rr & 3) + 8 * (rr >> 2);
-          float dv = d[0][0];  // d~ of this bit (select chain: no dynamic register indexing)
+        for (int kk = 0; kk < 8; ++kk) {
+          const int ko = kk * 16 + 8 * half;
+          const h8 thi = *reinterpret_cast<const h8*>(tH + trow + ko);
+          const h8 tlo = *reinterpret_cast<const h8*>(tL + trow + ko);
+          ahh = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qhi[kk], ahh, 0, 0, 0);
+          ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qlo[kk], ax, 0, 0, 0);
+          ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(tlo, qhi[kk], ax, 0, 0, 0);
+        }
+        // d~ = na + nb - 2 a.b with a.b = (ahh + ax 2^-11) 2^-16: two fmas by exact powers
+        // of two (each rounding is covered by E's 4e-6 (na + nb) term);
+        // targets past n2 are padding rows with norm2 = +inf: d~ = +inf
 #pragma unroll
-          for (int k = 1; k < 32; ++k) dv = (bit == k) ? d[k >> 4][k & 15] : dv;
-          if (slot < kCandCap) {
-            sCand[ql][slot] = (uint16_t)j;
-            sCandD[ql][slot] = bf16_down(dv);
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 nb4 = *reinterpret_cast<const float4*>(&sN[32 * sub + 8 * g4 + 4 * half]);
+          const float nbv[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int rr = 4 * g4 + e;
+            const float t2 = na + nbv[e];
+            const float dv = __builtin_fmaf(ax[rr], -1.4901161193847656e-08f /* -2^-26 */,
+                                            __builtin_fmaf(ahh[rr], -3.0517578125e-05f /* -2^-15 */, t2));
+            if (PH == 0) {  // running top-2 (b1 <= b2): b2 = med3(b1, b2, d), b1 = min(b1, d)
+              b2 = __builtin_amdgcn_fmed3f(b1, b2, dv);
+              b1 = __builtin_amdgcn_fmed3f(b1, dv, -INFINITY);
+            } else {
+              mm |= (dv <= thr) ? (1u << (16 * sub + rr)) : 0u;
+            }
           }
         }
       }
+      if (PH == 1 && __any(mm != 0u)) {  // wave-uniform: skip when no lane admits
+        if (live && mm) {  // reserve this lane's slots with one LDS atomic, then fill them
+          int slot = atomicAdd(&sCnt[ql], __popc(mm));
+          for (; mm; mm &= mm - 1, ++slot) {
+            const int bit = __builtin_ctz(mm), rr = bit & 15;
+            const int j = st * kTT2 + 32 * (bit >> 4) + 4 * half + (rr & 3) + 8 * (rr >> 2);
+            if (slot < kCandCap) sCand[ql][slot] = (uint16_t)j;
+          }
+        }
+      }
+      if (st + 1 < nst) {
+        __syncthreads();  // every wave is done with this stage's LDS rows
+        store_stage();
+        if (tid < kTT2) sN[tid] = nrm_next;
+      }
     }
-    if (st + 1 < nst) {
-      __syncthreads();  // every wave is done with this stage's LDS rows
-      store_stage();
-      if (tid < kTT2) sN[tid] = nrm_next;
-    }
-  }
-  {  // the row's final threshold (both halves merged)
+  };
+  sweep(std::integral_constant<int, 0>{});
+  {  // the row's final window (both halves of the wave merged)
     const float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
-    if (half == 0) sThr[ql] = fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + 2.0f * E;
+    thr = fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + 2.0f * E;
   }
-  __syncthreads();  // sweep done: the stage buffers become the re-rank scratch
-  if (ABL == 8 && admit_x == 0x7fffffffu) rows_out[0].col = 1;  // defeats dead-code elimination
+  __syncthreads();  // sweep 1's last stage consumed before sweep 2 overwrites the buffer
+  if (ABL == 8) {
+    if (thr == -1.0f) rows_out[0].col = 1;  // defeats dead-code elimination
+    return;
+  }
+  sweep(std::integral_constant<int, 1>{});
+  __syncthreads();  // sweeps done: the stage buffers become the re-rank scratch
   if (ABL != 0) return;
 
-  // exact re-rank of the collected candidates, flattened over the workgroup: row rl owns
-  // entries [sOff[rl], sOff[rl+1]) of the candidate list, every thread takes every 256th
-  // keep only the candidates inside the row's FINAL window (their stored d~ is rounded
-  // down, so no window member is dropped): the running threshold admitted ~3x more
+  // exact re-rank of every window member, flattened over the workgroup: row rl owns
+  // entries [sOff[rl], sOff[rl+1]); a row whose window overflowed its list goes to the
+  // overflow kernel instead
   if (tid < kQB) {
-    int c = sCnt[tid];
-    if (c <= kCandCap && row0 + tid < n1) {
-      const float t = sThr[tid];
-      int k = 0;
-      for (int s = 0; s < c; ++s) {
-        const uint16_t dd = sCandD[tid][s];
-        if (__uint_as_float((uint32_t)dd << 16) <= t) sCand[tid][k++] = sCand[tid][s];
-      }
-      sCnt[tid] = c = k;
+    const int c = sCnt[tid];
+    const bool ok = row0 + tid < n1 && c <= kCandCap;
+    sOff[tid + 1] = ok ? c : 0;
+    if (row0 + tid < n1 && c > kCandCap) {
+      const int k = atomicAdd(ovf_count, 1);
+      ovf_list[k] = make_int2(p, row0 + tid);
     }
-    sOff[tid + 1] = (c <= kCandCap && row0 + tid < n1) ? c : 0;
   }
   if (tid == 0) sOff[0] = 0;
   __syncthreads();
@@ -353,27 +341,32 @@ __global__ void __launch_bounds__(256) k_match_mfma(
   const int total = sOff[kQB];
   const float* A = desc + (int64_t)i1 * cap * 128;
   const float* Bd = desc + (int64_t)i2 * cap * 128;
-  for (int e = tid; e < total; e += 256) {
-    int lo = 0, hi = kQB;  // the row with sOff[row] <= e < sOff[row + 1]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (sOff[mid] <= e) lo = mid; else hi = mid;
+  float e1 = INFINITY, e2 = INFINITY;
+  int j1 = 0x7fffffff;
+  for (int c0 = 0; c0 < total; c0 += kScr) {
+    const int c1 = min(total, c0 + kScr);
+    for (int e = c0 + tid; e < c1; e += 256) {
+      int lo_ = 0, hi_ = kQB;  // the row with sOff[row] <= e < sOff[row + 1]
+      while (hi_ - lo_ > 1) {
+        const int mid = (lo_ + hi_) >> 1;
+        if (sOff[mid] <= e) lo_ = mid; else hi_ = mid;
+      }
+      const int rl = lo_, slot = e - sOff[rl];
+      sDex[e - c0] = exact_sqdist(A + (int64_t)(row0 + rl) * 128, Bd + (int64_t)sCand[rl][slot] * 128);
     }
-    const int rl = lo, slot = e - sOff[rl];
-    sDex[rl * kCandCap + slot] =
-        exact_sqdist(A + (int64_t)(row0 + rl) * 128, Bd + (int64_t)sCand[rl][slot] * 128);
+    __syncthreads();
+    if (tid < kQB) {  // this row's entries inside the chunk, (distance, index) order
+      const int s0 = max(sOff[tid], c0), s1 = min(sOff[tid + 1], c1);
+      for (int e = s0; e < s1; ++e) {
+        const float dd = sDex[e - c0];
+        const int j = sCand[tid][e - sOff[tid]];
+        if (dd < e1 || (dd == e1 && j < j1)) { e2 = e1; e1 = dd; j1 = j; }
+        else if (dd < e2) e2 = dd;
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
   if (tid < kQB && row0 + tid < n1 && sCnt[tid] <= kCandCap) {
-    float e1 = INFINITY, e2 = INFINITY;
-    int j1 = 0x7fffffff;
-    const int c = sCnt[tid];
-    for (int s = 0; s < c; ++s) {
-      const float dd = sDex[tid * kCandCap + s];
-      const int j = sCand[tid][s];
-      if (dd < e1 || (dd == e1 && j < j1)) { e2 = e1; e1 = dd; j1 = j; }
-      else if (dd < e2) e2 = dd;
-    }
     RowBest rb;
     rb.col = -1;
     rb.nndr = 0.0f;
@@ -384,33 +377,52 @@ __global__ void __launch_bounds__(256) k_match_mfma(
     }
     rows_out[(int64_t)p * max_rows + row0 + tid] = rb;
   }
-  // overflow rows: exact over every target (whole workgroup per row)
-  for (int rl = 0; rl < kQB; ++rl) {
-    if (sCnt[rl] <= kCandCap || row0 + rl >= n1) continue;  // uniform branch
+}
+
+// Rows whose window overflowed the LDS list (long runs of near-identical target
+// descriptors): exact distances to every target, one wavefront per row — lanes stride the
+// targets (the query row is a wave-uniform broadcast load), per-lane (distance, index)
+// top-2, then a shuffle merge.  Grid-stride over the list, so the launch needs no host
+// read of its length.
+__global__ void __launch_bounds__(256) k_match_overflow(const float* __restrict__ desc,
+                                                        const int32_t* __restrict__ count, int64_t cap,
+                                                        const int32_t* __restrict__ pairs, float ratio,
+                                                        RowBest* __restrict__ rows_out, int max_rows,
+                                                        const int* __restrict__ ovf_count,
+                                                        const int2* __restrict__ ovf_list) {
+  const int nov = *ovf_count;
+  const int lane = threadIdx.x & 63;
+  for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < nov; w += gridDim.x * 4) {
+    const int2 ent = ovf_list[w];
+    const int p = ent.x, row = ent.y;
+    const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
+    const int n2 = count[i2];
+    const float* A = desc + ((int64_t)i1 * cap + row) * 128;
+    const float* Bd = desc + (int64_t)i2 * cap * 128;
     float e1 = INFINITY, e2 = INFINITY;
     int j1 = 0x7fffffff;
-    for (int j = tid; j < n2; j += 256) {
-      const float dd = exact_sqdist(A + (int64_t)(row0 + rl) * 128, Bd + (int64_t)j * 128);
+    for (int j = lane; j < n2; j += 64) {
+      const float dd = exact_sqdist(A, Bd + (int64_t)j * 128);
       if (dd < e1 || (dd == e1 && j < j1)) { e2 = e1; e1 = dd; j1 = j; }
       else if (dd < e2) e2 = dd;
     }
-    sRed[tid] = e1; sRed[256 + tid] = e2; sRedJ[tid] = j1;  // sDex is dead by now
-    __syncthreads();
-    if (tid == 0) {
-      float B1 = INFINITY, B2 = INFINITY;
-      int J1 = 0x7fffffff;
-      for (int t = 0; t < 256; ++t) top2_merge(B1, J1, B2, sRed[t], sRedJ[t], sRed[256 + t]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const float o1 = __shfl_xor(e1, off), o2 = __shfl_xor(e2, off);
+      const int oj = __shfl_xor(j1, off);
+      top2_merge(e1, j1, e2, o1, oj, o2);
+    }
+    if (lane == 0) {
       RowBest rb;
       rb.col = -1;
       rb.nndr = 0.0f;
-      const float d1 = sqrtf(B1), d2 = sqrtf(B2);
+      const float d1 = sqrtf(e1), d2 = sqrtf(e2);
       if (d2 > 0.0f) {
         const float nndr = d1 / d2;
-        if (nndr <= ratio) { rb.col = J1; rb.nndr = nndr; }
+        if (nndr <= ratio) { rb.col = j1; rb.nndr = nndr; }
       }
-      rows_out[(int64_t)p * max_rows + row0 + rl] = rb;
+      rows_out[(int64_t)p * max_rows + row] = rb;
     }
-    __syncthreads();
   }
 }
 
@@ -425,22 +437,26 @@ void launch_match_prep(const float* desc, const int32_t* count, int nimg, int64_
 void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int64_t capP,
                        const _Float16* hi, const _Float16* lo, const float* norm2, const float* rnorm,
                        const unsigned int* imgmax, const int32_t* pairs, int P, float ratio,
-                       RowBest* rows, int max_rows, hipStream_t st) {
+                       RowBest* rows, int max_rows, int* ovf_count, int2* ovf_list, hipStream_t st) {
   static const int abl = [] {
     const char* e = getenv("SFMFEAT_MATCH_ABL");  // diagnostics only (tools/bench_match.py)
     return e ? atoi(e) : 0;
   }();
   const int qb = (max_rows + kQB - 1) / kQB;
   const dim3 grid((unsigned)(8 * ((P + 7) / 8) * qb));
+  (void)hipMemsetAsync(ovf_count, 0, sizeof(int), st);
   if (abl == 6)
     hipLaunchKernelGGL(k_match_mfma<6>, grid, dim3(256), 0, st, desc, count, cap, capP, hi, lo, norm2, rnorm, imgmax,
-                       pairs, P, ratio, rows, max_rows);
+                       pairs, P, ratio, rows, max_rows, ovf_count, ovf_list);
   else if (abl == 8)
     hipLaunchKernelGGL(k_match_mfma<8>, grid, dim3(256), 0, st, desc, count, cap, capP, hi, lo, norm2, rnorm, imgmax,
-                       pairs, P, ratio, rows, max_rows);
+                       pairs, P, ratio, rows, max_rows, ovf_count, ovf_list);
   else
     hipLaunchKernelGGL(k_match_mfma<0>, grid, dim3(256), 0, st, desc, count, cap, capP, hi, lo, norm2, rnorm, imgmax,
-                       pairs, P, ratio, rows, max_rows);
+                       pairs, P, ratio, rows, max_rows, ovf_count, ovf_list);
+  // the overflow list's length stays on the device: a fixed grid strides over it
+  hipLaunchKernelGGL(k_match_overflow, dim3(256), dim3(256), 0, st, desc, count, cap, pairs, ratio, rows, max_rows,
+                     ovf_count, ovf_list);
 }
 
 }  // namespace sfm

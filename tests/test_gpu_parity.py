@@ -149,10 +149,12 @@ def test_matcher_vs_oracle_sizes(n1, n2, ratio):
 
 
 @pytest.mark.parametrize("n1,n2,jit,ratio", [(10, 700, 0, 0.9), (10, 700, 1, 0.9), (40, 900, 0, 1.0),
-                                             (300, 300, 0, 0.8)])
+                                             (300, 300, 0, 0.8), (4, 1500, 0, 0.9), (4, 1500, 1, 1.0),
+                                             (200, 3000, 0, 0.9)])
 def test_matcher_duplicate_targets_overflow_path(n1, n2, jit, ratio):
     """Runs of identical / near-identical targets widen the prefilter window past the
-    per-row candidate list and exercise the exact full-row fallback."""
+    per-row candidate list (128) and exercise the exact full-row overflow kernel (n2 / n1
+    duplicates of each source row: 375 at (4, 1500))."""
     a, ha = synth.make_descriptor_table(n1, 7 + n1)
     b, _ = synth.make_descriptor_table(n2, 9 + n2, dup_of=ha, jitter=jit)
     q, _ = synth.make_descriptor_table(n1, 11 + n1, dup_of=ha, jitter=2)
