@@ -22,6 +22,7 @@ constexpr int kMedBits1 = 11;               // median digit 1 (histogrammed insi
 constexpr int kMedBins1 = 1 << kMedBits1;   // 2048 (digits 2 / 3 are 11 / 10 bits)
 constexpr int kTopkLdsCap = 8192;           // max keys sorted in LDS by the top-k kernel
 constexpr int kMaxMatchRows = 16384;        // max keypoints per image for the matcher sort
+constexpr int kMatchCandCap = 128;          // admitted targets per query row (MFMA matcher lists)
 constexpr int kCounterStride = 32;          // u64 per per-plane atomic counter (own 256-B line)
 
 // Per-plane state of the keypoint selection (NaiveSIFT.py:90-120).
@@ -220,6 +221,7 @@ void launch_match_prep(const float* desc, const int32_t* count, int nimg, int64_
 void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int64_t capP,
                        const _Float16* hi, const _Float16* lo, const float* norm2, const float* rnorm,
                        const unsigned int* imgmax, const int32_t* pairs, int P, float ratio,
-                       RowBest* rows, int max_rows, int* ovf_count, int2* ovf_list, hipStream_t st);
+                       RowBest* rows, int max_rows, uint32_t* cand, int32_t* cand_n, float* cand_thr,
+                       int* ovf_count, int2* ovf_list, hipStream_t st);
 
 }  // namespace sfm

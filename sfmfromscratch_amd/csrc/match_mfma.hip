@@ -30,7 +30,7 @@ constexpr int kQW = 32;                // query rows per wave
 constexpr int kWaves = 4;              // waves per workgroup
 constexpr int kQB = kQW * kWaves;      // 128 query rows per workgroup
 constexpr int kRowH = 128 + 8;         // padded fp16 row in LDS (272 B): conflict-free b128 reads
-constexpr int kCandCap = 128;          // window members per query row kept in LDS
+constexpr int kCandCap = kMatchCandCap;  // admitted targets per query row (global list)
 constexpr float kScale = 256.0f;       // operand pre-scale (2^8)
 constexpr float kLoScale = 2048.0f;    // lo part scale (2^11)
 
@@ -126,6 +126,12 @@ SFM_DEV float exact_sqdist(const float* __restrict__ a, const float* __restrict_
   return u0 + u1;
 }
 
+// d~ rounded DOWN to bf16 (kept as its top 16 bits): truncation for positive values;
+// negative values (|d~| within E of 0) become -inf, which always passes the filter
+SFM_DEV uint16_t bf16_down(float v) {
+  return v >= 0.0f ? (uint16_t)(__float_as_uint(v) >> 16) : (uint16_t)0xFF80u;
+}
+
 SFM_DEV void top2_merge(float& b1, int& j1, float& b2, float ob1, int oj1, float ob2) {
   if (ob1 < b1 || (ob1 == b1 && oj1 < j1)) {
     b2 = fminf(b1, ob2);
@@ -138,39 +144,34 @@ SFM_DEV void top2_merge(float& b1, int& j1, float& b2, float ob1, int oj1, float
 
 constexpr int kTT2 = 64;               // targets per LDS stage (two 32-target MFMA sub-tiles)
 constexpr int kStageHalves = kTT2 * kRowH;  // f16 elements per array per stage
-constexpr int kScr = 2 * kStageHalves / 2;  // re-rank scratch floats in the stage buffers (8704)
 
-// One workgroup = 4 waves x 32 query rows; two sweeps over the target table of the pair, in
+// One workgroup = 4 waves x 32 query rows; ONE sweep over the target table of the pair in
 // 64-row LDS stages (the next stage's hi/lo rows are loaded into registers while the
-// current stage's MFMAs run, then stored into the single LDS stage buffer):
-//   sweep 1: the running top-2 of d~ per row (two v_med3 per element) -> the row's FINAL
-//            window thr = b2~ + 2E (both halves of the wave merged);
-//   sweep 2: the same MFMAs; every target with d~ <= thr is appended to the row's LDS list
-//            (index only: the window is exact, so no approximate distance is kept and no
-//            post-filter runs; a ballot skips the append code for stages where no lane of
-//            the wave admits anything).
-// Every target inside the window is re-ranked with the reference's exact float32 distance
-// (flattened over the workgroup, in chunks through the stage buffers).  A row whose window
-// holds more than kCandCap targets is handed to k_match_overflow (global list).
+// current stage's MFMAs run, then stored into the single LDS stage buffer), software-
+// pipelined by 32-target sub-tile: the MFMAs of one sub-tile run beside the epilogue of
+// the previous one.  Per element the epilogue forms d~, updates the row's running top-2
+// (two v_med3) and admits the target when d~ <= thr, thr = b2~(so far) + 2E: this lane's
+// own b2~ after the sub-tile, capped by the wave-merged b2~ of the previous stage.  b2~
+// only decreases, so every running thr >= the final one and the admitted set contains
+// the row's final window (argument below).  Admitted target indices go to the row's list
+// in global memory (kCandCap entries); k_match_rerank recomputes them with the
+// reference's exact float32 distance; a row whose list overflowed goes to
+// k_match_overflow (exact over all targets).
 // The window argument: the targets achieving b1~ and b2~ have exact distances <= b1~ + E and
 // <= b2~ + E, so the exact second-smallest D2 <= b2~ + E; a target with exact d <= D2 has
 // d~ <= d + E <= b2~ + 2E.  Targets outside the window are strictly farther than D2.
-// ABL (timing builds only; results are wrong unless 0): 6 = no re-rank, 8 = no sweep 2
+// ABL (timing builds only; results are wrong unless 0): 9 = no epilogue, 10 = no MFMAs
 template <int ABL>
 __global__ void __launch_bounds__(256, 2) k_match_mfma(
-    const float* __restrict__ desc, const int32_t* __restrict__ count, int64_t cap, int64_t capP,
-    const _Float16* __restrict__ hi, const _Float16* __restrict__ lo, const float* __restrict__ norm2,
-    const float* __restrict__ rnorm, const unsigned int* __restrict__ imgmax,
-    const int32_t* __restrict__ pairs, int P, float ratio, RowBest* __restrict__ rows_out, int max_rows,
+    const int32_t* __restrict__ count, int64_t capP, const _Float16* __restrict__ hi,
+    const _Float16* __restrict__ lo, const float* __restrict__ norm2, const float* __restrict__ rnorm,
+    const unsigned int* __restrict__ imgmax, const int32_t* __restrict__ pairs, int P, int max_rows,
+    uint32_t* __restrict__ cand, int32_t* __restrict__ cand_n, float* __restrict__ cand_thr,
     int* __restrict__ ovf_count, int2* __restrict__ ovf_list) {
-  // stage buffer [hi|lo][64][kRowH]; after the sweeps the space holds the re-rank scratch
   __shared__ __attribute__((aligned(16))) _Float16 sT[2][kStageHalves];
-  __shared__ __attribute__((aligned(16))) float sN[kTT2];
-  __shared__ uint16_t sCand[kQB][kCandCap];
+  __shared__ __attribute__((aligned(16))) float sN[2][kTT2];  // target norms, by stage parity
   __shared__ int sCnt[kQB];
-  __shared__ int sOff[kQB + 1];
-  float* sDex = reinterpret_cast<float*>(&sT[0][0]);
-  static_assert(sizeof(sT) >= (size_t)kScr * 4, "re-rank scratch fits");
+  __shared__ __attribute__((aligned(16))) float sD[kWaves][64][16];  // a sub-tile's d~ per lane
 
   // XCD-aware mapping (workgroups b and b + 8 share an XCD and its L2): group g = b % 8
   // takes the pairs p = g (mod 8), so all query blocks of a pair stream its target table
@@ -202,171 +203,272 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
   const float maxrn = __uint_as_float(imgmax[i2 * 2 + 1]);
   // rigorous |d~ - d_ref| bound (matcher exactness)
   const float E = 3.0517578125e-05f * ra * maxrn + 4e-6f * (na + maxn2) + 1.25e-4f;
+  const float E2 = 2.0f * E;
   for (int i = tid; i < kQB; i += 256) sCnt[i] = 0;
+  const bool live = qi < n1;
+  uint32_t* my_list = cand + ((int64_t)p * max_rows + qi) * kCandCap;
 
   const int nst = (n2 + kTT2 - 1) / kTT2;
   const int64_t to = (int64_t)i2 * capP * 128;
-  // stage loader: 64 rows x (hi, lo) x 256 B = 32 KB; thread -> (row, 32-B column chunk)
-  const int lr = tid >> 2, lc = (tid & 3) * 32;   // row 0..63, halves 0..127 step 32
+  // stage loader: 64 rows x (hi, lo) x 256 B = 32 KB, each array one contiguous 16 KB run;
+  // pass q reads 4 KB of it with consecutive 16-B pieces per lane (one 1 KB run per wave
+  // instruction): thread t -> row 16 q + t / 16, halves 8 (t % 16)
+  const int lr = tid >> 4, lc = (tid & 15) * 8;
   h8 g[8];
   auto load_stage = [&](int st) {
-    const int64_t gofs = to + (int64_t)(st * kTT2 + lr) * 128 + lc;  // rows < capP: in bounds
+    const int64_t gofs = to + (int64_t)(st * kTT2) * 128 + tid * 8;  // rows < capP: in bounds
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      g[q] = *reinterpret_cast<const h8*>(hi + gofs + 8 * q);
-      g[4 + q] = *reinterpret_cast<const h8*>(lo + gofs + 8 * q);
+      g[q] = *reinterpret_cast<const h8*>(hi + gofs + 2048 * q);
+      g[4 + q] = *reinterpret_cast<const h8*>(lo + gofs + 2048 * q);
     }
   };
   auto store_stage = [&]() {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      *reinterpret_cast<h8*>(&sT[0][lr * kRowH + lc + 8 * q]) = g[q];
-      *reinterpret_cast<h8*>(&sT[1][lr * kRowH + lc + 8 * q]) = g[4 + q];
+      *reinterpret_cast<h8*>(&sT[0][(16 * q + lr) * kRowH + lc]) = g[q];
+      *reinterpret_cast<h8*>(&sT[1][(16 * q + lr) * kRowH + lc]) = g[4 + q];
+    }
+  };
+  // 32 targets x 32 queries of sub-tile `sub` of the staged rows: hi.hi into ahh, hi.lo +
+  // lo.hi into ax (one accumulation chain each)
+  auto mfma_sub = [&](int sub, f32x16& ahh, f32x16& ax) {
+    const _Float16* tH = &sT[0][0];
+    const _Float16* tL = &sT[1][0];
+    const int trow = (32 * sub + (lane & 31)) * kRowH;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int ko = kk * 16 + 8 * half;
+      const h8 thi = *reinterpret_cast<const h8*>(tH + trow + ko);
+      const h8 tlo = *reinterpret_cast<const h8*>(tL + trow + ko);
+      if (ABL == 10) {
+        asm volatile("" ::"v"(thi), "v"(tlo));
+        continue;
+      }
+      ahh = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qhi[kk], ahh, 0, 0, 0);
+      ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qlo[kk], ax, 0, 0, 0);
+      ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(tlo, qhi[kk], ax, 0, 0, 0);
+    }
+  };
+  // this lane's 16 target norms of sub-tile `sub` (MFMA row layout: 8 (rr >> 2) + 4 half + (rr & 3))
+  auto load_nb = [&](int par, int sub, float (&nb)[16]) {
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const float4 v = *reinterpret_cast<const float4*>(&sN[par][32 * sub + 8 * g4 + 4 * half]);
+      nb[4 * g4 + 0] = v.x; nb[4 * g4 + 1] = v.y; nb[4 * g4 + 2] = v.z; nb[4 * g4 + 3] = v.w;
+    }
+  };
+  float b1 = INFINITY, b2 = INFINITY;
+  float thr_w = 3.0e38f;  // wave-merged running threshold of the previous stage (finite:
+                          // padding targets, d~ = +inf, are never admitted)
+  // d~ = na + nb - 2 a.b with a.b = (ahh + ax 2^-11) 2^-16: two fmas by exact powers of two
+  // (each rounding is covered by E's 4e-6 (na + nb) term); padding targets
+  // have norm2 = +inf: d~ = +inf.  Running top-2 (b2 = med3(b1, b2, d), b1 = min), then
+  // bit rr of mm for d~ <= min(b2~ + 2E, thr_w)
+  auto epi = [&](const f32x16& ahh, const f32x16& ax, const float (&nb)[16], float (&d)[16], uint32_t& mm) {
+    if (ABL == 9) {
+      asm volatile("" ::"v"(ahh), "v"(ax));
+      return;
+    }
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) {
+      d[rr] = __builtin_fmaf(ax[rr], -1.4901161193847656e-08f /* -2^-26 */,
+                             __builtin_fmaf(ahh[rr], -3.0517578125e-05f /* -2^-15 */, na + nb[rr]));
+      b2 = __builtin_amdgcn_fmed3f(b1, b2, d[rr]);
+      b1 = __builtin_amdgcn_fmed3f(b1, d[rr], -INFINITY);
+    }
+    const float t = fminf(b2 + E2, thr_w);
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) mm |= (d[rr] <= t) ? (1u << rr) : 0u;
+  };
+  // MFMA / VALU interleave of one software-pipelined region: per k-step two fragment
+  // reads, then the three MFMAs with the epilogue's vector instructions in their gaps
+  auto interleave = [&]() {
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+    }
+  };
+  // the region's epilogue results are needed here: keeps the compiler from sinking the
+  // epilogue past the stage barrier, out of the region it interleaves with
+  auto pin = [](float x1, float x2, uint32_t mm) { asm volatile("" ::"v"(x1), "v"(x2), "v"(mm)); };
+  // admitted elements of one sub-tile (bit rr of mm, targets jb + 8 (rr >> 2) + 4 half +
+  // (rr & 3)) -> the row's global list as (index | d~ rounded down to bf16 << 16).  When
+  // any lane of the wave admits, the lane's 16 d~ go to its LDS row (4 x 16-B stores) and
+  // each admitted one is read back by index (no dynamic register indexing into d)
+  float* my_d = &sD[wid][lane][0];
+  auto append = [&](uint32_t mm, const float (&d)[16], int jb) {
+    if (__any(mm != 0u)) {  // wave-uniform: skip when no lane admits
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<float4*>(my_d + 4 * q) = make_float4(d[4 * q], d[4 * q + 1], d[4 * q + 2], d[4 * q + 3]);
+      if (live && mm) {  // reserve this lane's slots with one LDS atomic, then fill them
+        int slot = atomicAdd(&sCnt[ql], __popc(mm));
+        for (; mm; mm &= mm - 1, ++slot) {
+          const int rr = __builtin_ctz(mm);
+          if (slot < kCandCap)
+            my_list[slot] = (uint32_t)(jb + 4 * half + (rr & 3) + 8 * (rr >> 2)) | ((uint32_t)bf16_down(my_d[rr]) << 16);
+        }
+      }
     }
   };
 
-  float b1 = INFINITY, b2 = INFINITY, thr = INFINITY;
-  const bool live = qi < n1;
-  // one sweep over the pair's targets; PH 0 tracks the running top-2, PH 1 appends the
-  // final window
-  auto sweep = [&](auto phc) {
-    constexpr int PH = decltype(phc)::value;
-    load_stage(0);
-    const float nrm_t0 = (tid < kTT2) ? norm2[(int64_t)i2 * capP + tid] : 0.0f;
-    store_stage();
-    if (tid < kTT2) sN[tid] = nrm_t0;
-    for (int st = 0; st < nst; ++st) {
-      __syncthreads();  // stage st visible
-      float nrm_next = 0.0f;
-      if (st + 1 < nst) {
-        load_stage(st + 1);
-        if (tid < kTT2) nrm_next = norm2[(int64_t)i2 * capP + (st + 1) * kTT2 + tid];
-      }
-      const _Float16* tH = &sT[0][0];
-      const _Float16* tL = &sT[1][0];
-      uint32_t mm = 0;
-#pragma unroll
-      for (int sub = 0; sub < 2; ++sub) {
-        // 32 targets x 32 queries: hi.hi into ahh, hi.lo + lo.hi into ax (one chain each)
-        f32x16 ahh = {}, ax = {};
-        const int trow = (32 * sub + (lane & 31)) * kRowH;
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-          const int ko = kk * 16 + 8 * half;
-          const h8 thi = *reinterpret_cast<const h8*>(tH + trow + ko);
-          const h8 tlo = *reinterpret_cast<const h8*>(tL + trow + ko);
-          ahh = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qhi[kk], ahh, 0, 0, 0);
-          ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qlo[kk], ax, 0, 0, 0);
-          ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(tlo, qhi[kk], ax, 0, 0, 0);
-        }
-        // d~ = na + nb - 2 a.b with a.b = (ahh + ax 2^-11) 2^-16: two fmas by exact powers
-        // of two (each rounding is covered by E's 4e-6 (na + nb) term);
-        // targets past n2 are padding rows with norm2 = +inf: d~ = +inf
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const float4 nb4 = *reinterpret_cast<const float4*>(&sN[32 * sub + 8 * g4 + 4 * half]);
-          const float nbv[4] = {nb4.x, nb4.y, nb4.z, nb4.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int rr = 4 * g4 + e;
-            const float t2 = na + nbv[e];
-            const float dv = __builtin_fmaf(ax[rr], -1.4901161193847656e-08f /* -2^-26 */,
-                                            __builtin_fmaf(ahh[rr], -3.0517578125e-05f /* -2^-15 */, t2));
-            if (PH == 0) {  // running top-2 (b1 <= b2): b2 = med3(b1, b2, d), b1 = min(b1, d)
-              b2 = __builtin_amdgcn_fmed3f(b1, b2, dv);
-              b1 = __builtin_amdgcn_fmed3f(b1, dv, -INFINITY);
-            } else {
-              mm |= (dv <= thr) ? (1u << (16 * sub + rr)) : 0u;
-            }
-          }
-        }
-      }
-      if (PH == 1 && __any(mm != 0u)) {  // wave-uniform: skip when no lane admits
-        if (live && mm) {  // reserve this lane's slots with one LDS atomic, then fill them
-          int slot = atomicAdd(&sCnt[ql], __popc(mm));
-          for (; mm; mm &= mm - 1, ++slot) {
-            const int bit = __builtin_ctz(mm), rr = bit & 15;
-            const int j = st * kTT2 + 32 * (bit >> 4) + 4 * half + (rr & 3) + 8 * (rr >> 2);
-            if (slot < kCandCap) sCand[ql][slot] = (uint16_t)j;
-          }
-        }
-      }
-      if (st + 1 < nst) {
-        __syncthreads();  // every wave is done with this stage's LDS rows
-        store_stage();
-        if (tid < kTT2) sN[tid] = nrm_next;
-      }
-    }
-  };
-  sweep(std::integral_constant<int, 0>{});
-  {  // the row's final window (both halves of the wave merged)
-    const float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
-    thr = fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + 2.0f * E;
+  load_stage(0);
+  const float nrm_t0 = (tid < kTT2) ? norm2[(int64_t)i2 * capP + tid] : 0.0f;
+  store_stage();
+  if (tid < kTT2) {
+    sN[0][tid] = nrm_t0;
+    sN[1][tid] = INFINITY;  // "stage -1": the carried sub-tile's first epilogue is a no-op
   }
-  __syncthreads();  // sweep 1's last stage consumed before sweep 2 overwrites the buffer
-  if (ABL == 8) {
-    if (thr == -1.0f) rows_out[0].col = 1;  // defeats dead-code elimination
+  f32x16 ph_hh = {}, ph_x = {};  // carried sub-tile 1 of the previous stage
+  for (int st = 0; st < nst; ++st) {
+    __syncthreads();  // stage st visible
+    // next stage's rows (the last stage re-reads itself: branch-free loop body, so the
+    // MFMAs and the epilogue share one scheduling region)
+    const int sn = min(st + 1, nst - 1);
+    load_stage(sn);
+    const float nrm_next = norm2[(int64_t)i2 * capP + sn * kTT2 + (tid & (kTT2 - 1))];
+    const int par = st & 1;
+    {
+      float nb[16], d[16];
+      uint32_t mm = 0;
+      f32x16 h0 = {}, x0 = {};
+      load_nb(par ^ 1, 1, nb);
+      mfma_sub(0, h0, x0);
+      epi(ph_hh, ph_x, nb, d, mm);
+      interleave();
+      pin(b1, b2, mm);
+      append(mm, d, (st - 1) * kTT2 + 32);
+      ph_hh = h0;
+      ph_x = x0;
+    }
+    {
+      float nb[16], d[16];
+      uint32_t mm = 0;
+      f32x16 h1 = {}, x1 = {};
+      load_nb(par, 0, nb);
+      mfma_sub(1, h1, x1);
+      epi(ph_hh, ph_x, nb, d, mm);
+      interleave();
+      pin(b1, b2, mm);
+      append(mm, d, st * kTT2);
+      ph_hh = h1;
+      ph_x = x1;
+    }
+    {  // the wave-merged running threshold for the next stage (both halves of a row)
+      const float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
+      thr_w = fminf(fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + E2, thr_w);
+    }
+    __syncthreads();  // every wave is done with this stage's LDS rows and norms
+    store_stage();
+    if (tid < kTT2) sN[par ^ 1][tid] = nrm_next;
+  }
+  {
+    uint32_t mm = 0;  // the last stage's sub-tile 1
+    float nb[16], d[16];
+    load_nb((nst - 1) & 1, 1, nb);
+    epi(ph_hh, ph_x, nb, d, mm);
+    append(mm, d, (nst - 1) * kTT2 + 32);
+  }
+  // the row's final window threshold (both halves merged): the re-rank drops the admitted
+  // targets above it (their stored d~ is rounded down, so no window member is dropped)
+  const float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
+  const float thr_final = fminf(fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + E2, thr_w);
+  if (ABL != 0) {
+    if (thr_final == -1.0f) cand_n[0] = 1;  // defeats dead-code elimination
     return;
   }
-  sweep(std::integral_constant<int, 1>{});
-  __syncthreads();  // sweeps done: the stage buffers become the re-rank scratch
-  if (ABL != 0) return;
-
-  // exact re-rank of every window member, flattened over the workgroup: row rl owns
-  // entries [sOff[rl], sOff[rl+1]); a row whose window overflowed its list goes to the
-  // overflow kernel instead
-  if (tid < kQB) {
+  if (live && half == 0) cand_thr[(int64_t)p * max_rows + qi] = thr_final;
+  __syncthreads();
+  if (tid < kQB && row0 + tid < n1) {
     const int c = sCnt[tid];
-    const bool ok = row0 + tid < n1 && c <= kCandCap;
-    sOff[tid + 1] = ok ? c : 0;
-    if (row0 + tid < n1 && c > kCandCap) {
+    cand_n[(int64_t)p * max_rows + row0 + tid] = c;
+    if (c > kCandCap) {  // the list overflowed: exact over every target instead
       const int k = atomicAdd(ovf_count, 1);
       ovf_list[k] = make_int2(p, row0 + tid);
     }
   }
-  if (tid == 0) sOff[0] = 0;
-  __syncthreads();
-  if (tid < 64) {  // inclusive scan of the 128 counts by one wave (2 per lane)
-    int a = sOff[2 * tid + 1], b = sOff[2 * tid + 2];
-    int x = a + b;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(x, off);
-      if (tid >= off) x += y;
-    }
-    sOff[2 * tid + 1] = x - b;
-    sOff[2 * tid + 2] = x;
-  }
-  __syncthreads();
-  const int total = sOff[kQB];
-  const float* A = desc + (int64_t)i1 * cap * 128;
+}
+
+// Exact re-rank of the row's final window: the admitted targets whose stored d~ (rounded
+// down) is within the row's final threshold, compacted by a ballot into LDS, then the
+// reference's float32 distance (numpy's pairwise order) of each: one wavefront per query
+// row, eight lanes per candidate — lane l of a group accumulates numpy's accumulator
+// r[l] = sum_i (a[8 i + l] - b[8 i + l])^2 in i order (32-B coalesced reads per group),
+// and the groups' partial sums combine as ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
+// by xor shuffles (IEEE addition is commutative, so the shuffle pairing is bitwise the
+// reference's).  Per group a running (distance, index) top-2, merged over the 8 groups ->
+// nndr and the ratio test.
+__global__ void __launch_bounds__(256) k_match_rerank(const float* __restrict__ desc,
+                                                      const int32_t* __restrict__ count, int64_t cap,
+                                                      const int32_t* __restrict__ pairs, int P, float ratio,
+                                                      int max_rows, const uint32_t* __restrict__ cand,
+                                                      const int32_t* __restrict__ cand_n,
+                                                      const float* __restrict__ cand_thr,
+                                                      RowBest* __restrict__ rows_out) {
+  __shared__ uint16_t sJ[4][kCandCap];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int grp = lane >> 3, l8 = lane & 7;
+  const int64_t w = (int64_t)blockIdx.x * 4 + wv;  // (pair, row)
+  const int p = (int)(w / max_rows), row = (int)(w % max_rows);
+  if (p >= P) return;
+  const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
+  const int n1 = count[i1], n2 = count[i2];
+  if (row >= n1 || n2 < 1) return;
+  const int c = cand_n[w];
+  if (c > kCandCap) return;  // k_match_overflow's row
+  const float thr = cand_thr[w];
+  const uint32_t* list = cand + w * kCandCap;
+  const float* A = desc + ((int64_t)i1 * cap + row) * 128;
   const float* Bd = desc + (int64_t)i2 * cap * 128;
+  float a[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) a[i] = A[8 * i + l8];
+  int nk = 0;  // window members, compacted into sJ[wv] in list order
+  for (int s0 = 0; s0 < c; s0 += 64) {
+    const int s = s0 + lane;
+    const uint32_t e = s < c ? list[s] : 0u;
+    const bool keep = s < c && __uint_as_float(e & 0xffff0000u) <= thr;
+    const uint64_t bal = __ballot(keep);
+    if (keep) sJ[wv][nk + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(e & 0xffffu);
+    nk += __popcll(bal);
+  }
+  __builtin_amdgcn_wave_barrier();
   float e1 = INFINITY, e2 = INFINITY;
   int j1 = 0x7fffffff;
-  for (int c0 = 0; c0 < total; c0 += kScr) {
-    const int c1 = min(total, c0 + kScr);
-    for (int e = c0 + tid; e < c1; e += 256) {
-      int lo_ = 0, hi_ = kQB;  // the row with sOff[row] <= e < sOff[row + 1]
-      while (hi_ - lo_ > 1) {
-        const int mid = (lo_ + hi_) >> 1;
-        if (sOff[mid] <= e) lo_ = mid; else hi_ = mid;
-      }
-      const int rl = lo_, slot = e - sOff[rl];
-      sDex[e - c0] = exact_sqdist(A + (int64_t)(row0 + rl) * 128, Bd + (int64_t)sCand[rl][slot] * 128);
+  for (int s0 = 0; s0 < nk; s0 += 8) {
+    const int s = s0 + grp;
+    const bool ok = s < nk;
+    const int j = ok ? (int)sJ[wv][s] : 0;
+    const float* b = Bd + (int64_t)j * 128;
+    float r = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float dd = a[i] - b[8 * i + l8];
+      const float sq = dd * dd;
+      r = (i == 0) ? sq : r + sq;
     }
-    __syncthreads();
-    if (tid < kQB) {  // this row's entries inside the chunk, (distance, index) order
-      const int s0 = max(sOff[tid], c0), s1 = min(sOff[tid + 1], c1);
-      for (int e = s0; e < s1; ++e) {
-        const float dd = sDex[e - c0];
-        const int j = sCand[tid][e - sOff[tid]];
-        if (dd < e1 || (dd == e1 && j < j1)) { e2 = e1; e1 = dd; j1 = j; }
-        else if (dd < e2) e2 = dd;
-      }
+    r = r + __shfl_xor(r, 1);  // t01, t23, t45, t67
+    r = r + __shfl_xor(r, 2);  // u0 = t01 + t23, u1 = t45 + t67
+    r = r + __shfl_xor(r, 4);  // u0 + u1
+    if (ok) {
+      if (r < e1 || (r == e1 && j < j1)) { e2 = e1; e1 = r; j1 = j; }
+      else if (r < e2) e2 = r;
     }
-    __syncthreads();
   }
-  if (tid < kQB && row0 + tid < n1 && sCnt[tid] <= kCandCap) {
+#pragma unroll
+  for (int off = 8; off <= 32; off <<= 1) {
+    const float o1 = __shfl_xor(e1, off), o2 = __shfl_xor(e2, off);
+    const int oj = __shfl_xor(j1, off);
+    top2_merge(e1, j1, e2, o1, oj, o2);
+  }
+  if (lane == 0) {
     RowBest rb;
     rb.col = -1;
     rb.nndr = 0.0f;
@@ -375,7 +477,7 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
       const float nndr = d1 / d2;
       if (nndr <= ratio) { rb.col = j1; rb.nndr = nndr; }
     }
-    rows_out[(int64_t)p * max_rows + row0 + tid] = rb;
+    rows_out[w] = rb;
   }
 }
 
@@ -437,7 +539,8 @@ void launch_match_prep(const float* desc, const int32_t* count, int nimg, int64_
 void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int64_t capP,
                        const _Float16* hi, const _Float16* lo, const float* norm2, const float* rnorm,
                        const unsigned int* imgmax, const int32_t* pairs, int P, float ratio,
-                       RowBest* rows, int max_rows, int* ovf_count, int2* ovf_list, hipStream_t st) {
+                       RowBest* rows, int max_rows, uint32_t* cand, int32_t* cand_n, float* cand_thr,
+                       int* ovf_count, int2* ovf_list, hipStream_t st) {
   static const int abl = [] {
     const char* e = getenv("SFMFEAT_MATCH_ABL");  // diagnostics only (tools/bench_match.py)
     return e ? atoi(e) : 0;
@@ -445,18 +548,24 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
   const int qb = (max_rows + kQB - 1) / kQB;
   const dim3 grid((unsigned)(8 * ((P + 7) / 8) * qb));
   (void)hipMemsetAsync(ovf_count, 0, sizeof(int), st);
-  if (abl == 6)
-    hipLaunchKernelGGL(k_match_mfma<6>, grid, dim3(256), 0, st, desc, count, cap, capP, hi, lo, norm2, rnorm, imgmax,
-                       pairs, P, ratio, rows, max_rows, ovf_count, ovf_list);
-  else if (abl == 8)
-    hipLaunchKernelGGL(k_match_mfma<8>, grid, dim3(256), 0, st, desc, count, cap, capP, hi, lo, norm2, rnorm, imgmax,
-                       pairs, P, ratio, rows, max_rows, ovf_count, ovf_list);
+#define SFM_SWEEP(A)                                                                                           \
+  hipLaunchKernelGGL(k_match_mfma<A>, grid, dim3(256), 0, st, count, capP, hi, lo, norm2, rnorm, imgmax, pairs, P, \
+                     max_rows, cand, cand_n, cand_thr, ovf_count, ovf_list)
+  if (abl == 9)
+    SFM_SWEEP(9);
+  else if (abl == 10)
+    SFM_SWEEP(10);
   else
-    hipLaunchKernelGGL(k_match_mfma<0>, grid, dim3(256), 0, st, desc, count, cap, capP, hi, lo, norm2, rnorm, imgmax,
-                       pairs, P, ratio, rows, max_rows, ovf_count, ovf_list);
-  // the overflow list's length stays on the device: a fixed grid strides over it
-  hipLaunchKernelGGL(k_match_overflow, dim3(256), dim3(256), 0, st, desc, count, cap, pairs, ratio, rows, max_rows,
-                     ovf_count, ovf_list);
+    SFM_SWEEP(0);
+#undef SFM_SWEEP
+  if (abl == 0 || abl == 6) {  // 6: no re-rank (timing)
+    if (abl == 0)
+      hipLaunchKernelGGL(k_match_rerank, dim3((unsigned)(((int64_t)P * max_rows + 3) / 4)), dim3(256), 0, st, desc,
+                         count, cap, pairs, P, ratio, max_rows, cand, cand_n, cand_thr, rows);
+    // the overflow list's length stays on the device: a fixed grid strides over it
+    hipLaunchKernelGGL(k_match_overflow, dim3(256), dim3(256), 0, st, desc, count, cap, pairs, ratio, rows,
+                       max_rows, ovf_count, ovf_list);
+  }
 }
 
 }  // namespace sfm

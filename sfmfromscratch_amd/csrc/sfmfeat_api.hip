@@ -54,7 +54,7 @@ struct sfm_ctx {
   DevBuf d_gauss, d_img0, d_lvl, d_R, d_hist, d_med, d_medlist, d_counts, d_cand, d_scratch,
       d_kpx, d_kpy, d_kpc, d_lc, d_xy, d_desc, d_conf, d_count, d_u8;
   DevBuf m_desc, m_count, m_pairs, m_descT, m_rows, m_matches, m_conf, m_nmatch;
-  DevBuf m_hi, m_lo, m_norm2, m_rnorm, m_imgmax, m_ovf, m_ovfc;
+  DevBuf m_hi, m_lo, m_norm2, m_rnorm, m_imgmax, m_ovf, m_ovfc, m_cand, m_candn, m_candt;
   // ingest (sfm_ingest_rgb*): resample tables for the cached (W -> W2, H -> H2) and the
   // RGB temp of the horizontal pass; host staging for the host-pointer variant
   DevBuf i_tab_h, i_tab_v, i_tmp, i_rgb, i_gray;
@@ -419,6 +419,11 @@ int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, in
   if ((rc = ensure(c, c->m_rows, (size_t)P * cap * sizeof(RowBest)))) return rc;
   if ((rc = ensure(c, c->m_ovf, (size_t)P * cap * sizeof(int2)))) return rc;
   if ((rc = ensure(c, c->m_ovfc, 16))) return rc;
+  if (!c->match_direct) {  // admitted-target lists of the MFMA sweep (kMatchCandCap per row)
+    if ((rc = ensure(c, c->m_cand, (size_t)P * cap * kMatchCandCap * 4))) return rc;
+    if ((rc = ensure(c, c->m_candn, (size_t)P * cap * 4))) return rc;
+    if ((rc = ensure(c, c->m_candt, (size_t)P * cap * 4))) return rc;
+  }
   if (c->match_direct) {
     const int64_t capP = (cap + 63) / 64 * 64;
     StageScope sc(c, SFM_PROF_MATCH, st);
@@ -428,7 +433,8 @@ int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, in
     StageScope sc(c, SFM_PROF_MATCH, st);
     launch_match_mfma(desc, count, cap, capP, as<_Float16>(c->m_hi), as<_Float16>(c->m_lo), as<float>(c->m_norm2),
                       as<float>(c->m_rnorm), as<unsigned int>(c->m_imgmax), pairs, P, ratio, as<RowBest>(c->m_rows),
-                      (int)cap, as<int>(c->m_ovfc), as<int2>(c->m_ovf), st);
+                      (int)cap, as<uint32_t>(c->m_cand), as<int32_t>(c->m_candn), as<float>(c->m_candt), as<int>(c->m_ovfc),
+                      as<int2>(c->m_ovf), st);
   }
   {
     StageScope sc(c, SFM_PROF_MATCH_POST, st);
@@ -549,7 +555,7 @@ int32_t sfm_ctx_destroy(sfm_ctx* c) {
                     &c->d_counts, &c->d_cand, &c->d_scratch, &c->d_kpx, &c->d_kpy, &c->d_kpc, &c->d_lc,
                     &c->d_xy, &c->d_desc, &c->d_conf, &c->d_count, &c->d_u8, &c->m_desc, &c->m_count, &c->m_pairs,
                     &c->m_descT, &c->m_rows, &c->m_matches, &c->m_conf, &c->m_nmatch,
-                    &c->m_hi, &c->m_lo, &c->m_norm2, &c->m_rnorm, &c->m_imgmax, &c->m_ovf, &c->m_ovfc,
+                    &c->m_hi, &c->m_lo, &c->m_norm2, &c->m_rnorm, &c->m_imgmax, &c->m_ovf, &c->m_ovfc, &c->m_cand, &c->m_candn, &c->m_candt,
                     &c->i_tab_h, &c->i_tab_v, &c->i_tmp, &c->i_rgb, &c->i_gray, &c->i_colmap, &c->i_sets,
                     &c->r_idx, &c->r_off, &c->r_F, &c->r_counts, &c->r_pts, &c->r_npts, &c->r_out, &c->r_on,
                     &c->r_oit};
