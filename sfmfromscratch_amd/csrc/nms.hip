@@ -13,11 +13,13 @@
 // "R == window max" is tested as "no cell of the clipped window is larger"; out-of-image
 // cells hold -inf and never win.
 //
-// k_nms_tile (ksize <= 9): persistent workgroups walk 64 x 64 tiles of one plane; the tile
-// + halo (72-float rows, 16-B aligned) is loaded with 16-B loads into registers one tile
-// ahead, then staged through LDS.  HBM-bound: ~1.2 reads of R.
+// k_nms_tile (ksize <= 9): persistent workgroups walk contiguous row-major runs of 64 x 64
+// tiles of one plane; the tile + halo (72-float rows, 16-B aligned) is loaded with 16-B
+// loads into registers one tile ahead, then staged through LDS.  HBM-bound: ~1.03 reads
+// of R (the column halo's lines are the neighbour tiles', fetched by the same workgroup).
 // k_nms_generic (larger ksize): separable window max on an LDS tile.
 #include <algorithm>
+#include <type_traits>
 
 #include "kernels.h"
 
@@ -86,8 +88,14 @@ __global__ void __launch_bounds__(256) k_nms_tile(const float* __restrict__ R,
   static_assert(VEC ? PER <= 32 : PER <= 8, "prefetch mask bits");
 
   const int c0 = (tid & 7) * 8;    // 8 output columns, rows tid >> 3 and (tid >> 3) + 32
-  if (blockIdx.x < ntiles) prefetch(blockIdx.x);
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // one workgroup per band of tile rows, walking its tiles left to right: a tile's column
+  // halo lies in the 128-B lines of its neighbours, which this workgroup fetches next (or
+  // just did) through the same L2 instead of another XCD's — the strided assignment of
+  // adjacent tiles to different workgroups fetched those lines twice
+  const int t_lo = (int)((int64_t)ntiles * blockIdx.x / gridDim.x);
+  const int t_hi = (int)((int64_t)ntiles * (blockIdx.x + 1) / gridDim.x);
+  if (t_lo < t_hi) prefetch(t_lo);
+  for (int tile = t_lo; tile < t_hi; ++tile) {
     const int tx0 = (tile % tiles_x) * kNT_W;
     const int ty0 = (tile / tiles_x) * kTT_H;
     __syncthreads();  // previous tile's LDS reads done
@@ -106,7 +114,7 @@ __global__ void __launch_bounds__(256) k_nms_tile(const float* __restrict__ R,
       if (e < NV4) reinterpret_cast<float4*>(&s_t[0][0])[e] = v;
     }
     __syncthreads();
-    if (tile + (int)gridDim.x < ntiles) prefetch(tile + gridDim.x);
+    if (tile + 1 < t_hi) prefetch(tile + 1);
     uint32_t flags = 0;
     float vals[16];
     // pixel q of this thread: KH == 1 -> 4 x 4 block (rows 4rg + q/4, columns 4cg + q%4);
@@ -257,6 +265,8 @@ template <int KH>
 static void launch_tile(const float* R, const MedianState* state, uint64_t* cand, unsigned long long* cnt,
                         int B, int H, int W, int tiles_x, int mode, hipStream_t st) {
   const int ntiles = tiles_x * ((H + kTT_H - 1) / kTT_H);
+  // contiguous row-major tile ranges per workgroup (enough workgroups to keep the bytes in
+  // flight: each holds one tile of prefetch)
   dim3 grid(std::min(ntiles, kNmsBlocksPerPlane), B);
   const bool vec = (W & 3) == 0;
   if (mode == 0 && vec)

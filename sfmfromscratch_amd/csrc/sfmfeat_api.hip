@@ -315,8 +315,10 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     const int h = lv[l].h, w = lv[l].w;
     if (!e.exact) {
       StageScope sc(c, SFM_PROF_TOPK, s);
-      launch_topk(e.cand, candcnt + e.co, as<uint64_t>(c->d_scratch), e.kp, std::max(c->kcap, 1), c->kcap, B, h, w,
-                  lv[l].fw / 2, e.med, 0, s);
+      // the scratch region of this level's stream (the aux stream's levels and the caller
+      // stream's levels select concurrently)
+      launch_topk(e.cand, candcnt + e.co, as<uint64_t>(c->d_scratch) + (l < L_aux ? 0 : (int64_t)B * H * W), e.kp,
+                  std::max(c->kcap, 1), c->kcap, B, h, w, lv[l].fw / 2, e.med, 0, s);
     }
     {
       StageScope sc(c, SFM_PROF_MEDIAN, s);
