@@ -132,10 +132,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ngpu = torch.cuda.device_count()
+    torch.cuda.set_device(local % max(ngpu, 1))
+    dev = torch.device("cuda", local % max(ngpu, 1))
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # BENCH_DIST_BACKEND=gloo: rehearsal of the multi-rank code paths with several ranks
+        # on one GPU (RCCL needs one GPU per rank); measurements use RCCL
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     if args.workload == "c3":
         return run_all_pairs(args, torch, dev)
@@ -168,7 +175,7 @@ def main():
     pairs = torch.from_numpy(pairs_np).to(dev)
     P = pairs.shape[0]
     # slot B of each lane's table = the next rank's first frame (halo)
-    pipe = BatchPipeline(P_OCT, RATIO, B, H, W, pairs, inflight=args.inflight, device=local, extra_slots=1)
+    pipe = BatchPipeline(P_OCT, RATIO, B, H, W, pairs, inflight=args.inflight, device=dev.index, extra_slots=1)
     ctxs = pipe.contexts
 
     def halo(slots, n):
