@@ -298,7 +298,8 @@ def main():
     if dom:
         # the dominant stage's launches inside the timed region, timed by their own events
         traffic = {}
-        if os.path.exists(TRAFFIC_FILE):
+        # the committed PMC traffic was measured on the headline workload (c2) only
+        if os.path.exists(TRAFFIC_FILE) and args.workload == "c2" and not args.rgb_ingest:
             with open(TRAFFIC_FILE) as f:
                 traffic = json.load(f).get("bytes_per_launch", {})
         bound, amount, unit, peak, abytes = stage_work(counts, args.steps)[dom]
@@ -616,11 +617,12 @@ def run_gather(args, torch, dist, dev, rank, world):
         dt = (time.perf_counter() - t0) / reps
         sent = S * slot_bytes
         gathered = n_global * slot_bytes
-        comm = {"kind": "all_gather_into_tensor x3 fields per chunk (RCCL)", "chunks": C,
+        comm = {"kind": f"all_gather_into_tensor x3 fields per chunk ({dist.get_backend()})", "chunks": C,
                 "bytes_sent_per_rank": sent, "bytes_gathered_per_rank": gathered,
                 "ms_alone": round(dt * 1e3, 3), "algbw_GBps": round(gathered / dt / 1e9, 1)}
     elif world > 1:
-        comm = {"kind": "halo: 1 slot point-to-point (RCCL send/recv)", "bytes_sent_per_rank": slot_bytes}
+        comm = {"kind": f"halo: 1 slot point-to-point send/recv ({dist.get_backend()})",
+                "bytes_sent_per_rank": slot_bytes}
 
     if world > 1:
         dist.barrier()
