@@ -281,15 +281,18 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
 #pragma unroll
     for (int rr = 0; rr < 16; ++rr) mm |= (d[rr] <= t) ? (1u << rr) : 0u;
   };
-  // MFMA / VALU interleave of one software-pipelined region: per k-step two fragment
-  // reads, then the three MFMAs with the epilogue's vector instructions in their gaps
+  // MFMA / VALU interleave of one software-pipelined region: the three MFMAs of a k-step
+  // with the epilogue's vector instructions in their gaps
   auto interleave = [&]() {
+    // fragment reads run two k-steps ahead of the MFMAs that consume them, so no MFMA
+    // waits on an LDS read issued just before it
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // DS read: k-steps 0 and 1
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
       __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if (kk < 6) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read: k-step kk + 2
       __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
