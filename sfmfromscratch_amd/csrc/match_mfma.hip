@@ -484,6 +484,134 @@ __global__ void __launch_bounds__(256) k_match_rerank(const float* __restrict__ 
   }
 }
 
+// Exact re-rank, eight (pair, row) items per wavefront: for launches of few pairs (the
+// consecutive schedule's 31), where k_match_rerank's wave per row leaves most lanes idle
+// and pays three dependent memory latencies per row with too few waves to hide them; at
+// thousands of pairs (all-pairs chunks) k_match_rerank keeps more loads in flight:
+//   1. the eight rows' counts and final thresholds (lanes 0-7), their list entries (the
+//      eight 512-B lists are contiguous: 16 coalesced loads per lane) and their query rows
+//      (into LDS) are fetched together;
+//   2. the entries whose stored d~ (rounded down) lies within the row's final threshold
+//      are compacted by ballots into the wave's LDS list, in row order;
+//   3. eight lanes per candidate compute the reference's float32 distance (numpy's
+//      pairwise order: lane l accumulates r[l] = sum_i (a[8 i + l] - b[8 i + l])^2 in i
+//      order, and the group combines ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) by
+//      xor shuffles — IEEE addition is commutative, so the pairing is bitwise numpy's);
+//   4. lane r scans row r's contiguous range of distances for the (distance, index)
+//      top-2 -> nndr and the ratio test.
+constexpr int kRrRows = 8;             // (pair, row) items per wavefront
+constexpr int kRerank8MaxPairs = 256;  // launches up to this many pairs take k_match_rerank8
+__global__ void __launch_bounds__(256) k_match_rerank8(const float* __restrict__ desc,
+                                                      const int32_t* __restrict__ count, int64_t cap,
+                                                      const int32_t* __restrict__ pairs, int P, float ratio,
+                                                      int max_rows, const uint32_t* __restrict__ cand,
+                                                      const int32_t* __restrict__ cand_n,
+                                                      const float* __restrict__ cand_thr,
+                                                      RowBest* __restrict__ rows_out) {
+  __shared__ __attribute__((aligned(16))) float sA[4][kRrRows][128];  // query rows
+  __shared__ uint16_t sL[4][kRrRows * kCandCap];  // window members (target index), row order
+  __shared__ float sDist[4][kRrRows * kCandCap];
+  __shared__ int sBeg[4][kRrRows + 1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int grp = lane >> 3, l8 = lane & 7;
+  const int64_t total = (int64_t)P * max_rows;
+  const int64_t w0 = ((int64_t)blockIdx.x * 4 + wv) * kRrRows;  // first (pair, row) item
+  if (w0 >= total) return;
+  // 1. per-row state on lanes 0..7, then broadcast by shuffles
+  int c_l = 0, ok_l = 0, i1_l = 0, i2_l = 0, row_l = 0, p_l = 0;
+  float thr_l = 0.0f;
+  if (lane < kRrRows) {
+    const int64_t w = w0 + lane;
+    if (w < total) {
+      p_l = (int)(w / max_rows);
+      row_l = (int)(w % max_rows);
+      i1_l = pairs[2 * p_l];
+      i2_l = pairs[2 * p_l + 1];
+      const int n1 = count[i1_l], n2 = count[i2_l];
+      if (row_l < n1 && n2 >= 1) {
+        c_l = cand_n[w];
+        thr_l = cand_thr[w];
+        ok_l = c_l <= kCandCap ? 1 : 0;  // overflowed rows belong to k_match_overflow
+      }
+    }
+    if (!ok_l) c_l = 0;
+  }
+  // query rows of the eight items -> LDS (row r: 128 floats; 16 per lane)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = lane * 4 + 256 * q;  // float index in [0, 1024)
+    const int r = e >> 7, k = e & 127;
+    const int ir = __shfl(i1_l, r), rr = __shfl(row_l, r), okr = __shfl(ok_l, r);
+    float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (okr) v = *reinterpret_cast<const float4*>(desc + ((int64_t)ir * cap + rr) * 128 + k);
+    *reinterpret_cast<float4*>(&sA[wv][r][k]) = v;
+  }
+  // 2. list entries of the eight rows (contiguous), filtered and compacted in row order
+  const uint32_t* lists = cand + w0 * kCandCap;
+  int nk = 0;
+#pragma unroll 4
+  for (int sidx = 0; sidx < kRrRows * kCandCap / 64; ++sidx) {
+    const int e = sidx * 64 + lane;
+    const int r = e / kCandCap, pos = e % kCandCap;  // r is wave-uniform per sidx
+    const int cr = __shfl(c_l, r);
+    const float tr = __shfl(thr_l, r);
+    const bool valid = pos < cr && w0 + r < total;
+    const uint32_t ent = valid ? lists[e] : 0u;
+    const bool keep = valid && __uint_as_float(ent & 0xffff0000u) <= tr;
+    const uint64_t bal = __ballot(keep);
+    if (pos == 0 && lane == (sidx * 64) % 64 && (e % kCandCap) == 0) sBeg[wv][r] = nk;  // row start
+    if (keep) sL[wv][nk + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(ent & 0xffffu);
+    nk += __popcll(bal);
+  }
+  if (lane == 0) sBeg[wv][kRrRows] = nk;
+  __builtin_amdgcn_wave_barrier();
+  // 3. exact distances, eight candidates per iteration
+  for (int s0 = 0; s0 < nk; s0 += 8) {
+    const int s = s0 + grp;
+    const bool ok = s < nk;
+    const int j = ok ? (int)sL[wv][s] : 0;
+    int r = 0;  // the entry's row: ranges [sBeg[r], sBeg[r + 1]) are in row order
+#pragma unroll
+    for (int k = 1; k < kRrRows; ++k) r += (s >= sBeg[wv][k]) ? 1 : 0;
+    const int i2 = __shfl(i2_l, r);
+    const float* b = desc + ((int64_t)i2 * cap + j) * 128;
+    const float* a = &sA[wv][r][0];
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float dd = a[8 * i + l8] - (ok ? b[8 * i + l8] : a[8 * i + l8]);
+      const float sq = dd * dd;
+      acc = (i == 0) ? sq : acc + sq;
+    }
+    acc = acc + __shfl_xor(acc, 1);  // t01, t23, t45, t67
+    acc = acc + __shfl_xor(acc, 2);  // u0 = t01 + t23, u1 = t45 + t67
+    acc = acc + __shfl_xor(acc, 4);  // u0 + u1
+    if (ok && l8 == 0) sDist[wv][s] = acc;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // 4. lane r: row r's top-2 over its contiguous range
+  if (lane < kRrRows && ok_l) {
+    float e1 = INFINITY, e2 = INFINITY;
+    int j1 = 0x7fffffff;
+    const int beg = sBeg[wv][lane], end = lane + 1 < kRrRows ? sBeg[wv][lane + 1] : nk;
+    for (int s = beg; s < end; ++s) {
+      const float dd = sDist[wv][s];
+      const int j = (int)sL[wv][s];
+      if (dd < e1 || (dd == e1 && j < j1)) { e2 = e1; e1 = dd; j1 = j; }
+      else if (dd < e2) e2 = dd;
+    }
+    RowBest rb;
+    rb.col = -1;
+    rb.nndr = 0.0f;
+    const float d1 = sqrtf(e1), d2 = sqrtf(e2);
+    if (d2 > 0.0f) {
+      const float nndr = d1 / d2;
+      if (nndr <= ratio) { rb.col = j1; rb.nndr = nndr; }
+    }
+    rows_out[w0 + lane] = rb;
+  }
+}
+
 // Rows whose window overflowed the LDS list (long runs of near-identical target
 // descriptors): exact distances to every target, one wavefront per row — lanes stride the
 // targets (the query row is a wave-uniform broadcast load), per-lane (distance, index)
@@ -562,7 +690,10 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
     SFM_SWEEP(0);
 #undef SFM_SWEEP
   if (abl == 0 || abl == 6) {  // 6: no re-rank (timing)
-    if (abl == 0)
+    if (abl == 0 && P <= kRerank8MaxPairs)
+      hipLaunchKernelGGL(k_match_rerank8, dim3((unsigned)(((int64_t)P * max_rows + 4 * kRrRows - 1) / (4 * kRrRows))),
+                         dim3(256), 0, st, desc, count, cap, pairs, P, ratio, max_rows, cand, cand_n, cand_thr, rows);
+    else if (abl == 0)
       hipLaunchKernelGGL(k_match_rerank, dim3((unsigned)(((int64_t)P * max_rows + 3) / 4)), dim3(256), 0, st, desc,
                          count, cap, pairs, P, ratio, max_rows, cand, cand_n, cand_thr, rows);
     // the overflow list's length stays on the device: a fixed grid strides over it
