@@ -484,10 +484,9 @@ __global__ void __launch_bounds__(256) k_match_rerank(const float* __restrict__ 
   }
 }
 
-// Exact re-rank, eight (pair, row) items per wavefront: for launches of few pairs (the
-// consecutive schedule's 31), where k_match_rerank's wave per row leaves most lanes idle
-// and pays three dependent memory latencies per row with too few waves to hide them; at
-// thousands of pairs (all-pairs chunks) k_match_rerank keeps more loads in flight:
+// Exact re-rank, eight (pair, row) items per wavefront (A/B variant, kRerank8MaxPairs):
+// for launches of few pairs k_match_rerank's wave per row leaves most lanes idle and pays
+// three dependent memory latencies per row with few waves to hide them:
 //   1. the eight rows' counts and final thresholds (lanes 0-7), their list entries (the
 //      eight 512-B lists are contiguous: 16 coalesced loads per lane) and their query rows
 //      (into LDS) are fetched together;
@@ -500,7 +499,12 @@ __global__ void __launch_bounds__(256) k_match_rerank(const float* __restrict__ 
 //   4. lane r scans row r's contiguous range of distances for the (distance, index)
 //      top-2 -> nndr and the ratio test.
 constexpr int kRrRows = 8;             // (pair, row) items per wavefront
-constexpr int kRerank8MaxPairs = 256;  // launches up to this many pairs take k_match_rerank8
+// launches of up to this many pairs take k_match_rerank8 (default 0: off).  Alone, a
+// 31-pair match call measured 0.291 ms with it against 0.382 (tools/bench_match.py), but
+// inside bench.py's pipeline the match stage measured 0.253 vs 0.222 ms and the headline
+// 29.7k vs 30.9k img/s, so the wave-per-row kernel is the default; SFMFEAT_RERANK8_MAX=N
+// switches it on for A/B timing
+constexpr int kRerank8MaxPairs = 0;
 __global__ void __launch_bounds__(256) k_match_rerank8(const float* __restrict__ desc,
                                                       const int32_t* __restrict__ count, int64_t cap,
                                                       const int32_t* __restrict__ pairs, int P, float ratio,
@@ -676,6 +680,10 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
     const char* e = getenv("SFMFEAT_MATCH_ABL");  // diagnostics only (tools/bench_match.py)
     return e ? atoi(e) : 0;
   }();
+  static const int rr8_max = [] {  // SFMFEAT_RERANK8_MAX: pair-count switch (A/B timing)
+    const char* e = getenv("SFMFEAT_RERANK8_MAX");
+    return e ? atoi(e) : kRerank8MaxPairs;
+  }();
   const int qb = (max_rows + kQB - 1) / kQB;
   const dim3 grid((unsigned)(8 * ((P + 7) / 8) * qb));
   (void)hipMemsetAsync(ovf_count, 0, sizeof(int), st);
@@ -690,7 +698,7 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
     SFM_SWEEP(0);
 #undef SFM_SWEEP
   if (abl == 0 || abl == 6) {  // 6: no re-rank (timing)
-    if (abl == 0 && P <= kRerank8MaxPairs)
+    if (abl == 0 && P <= rr8_max)
       hipLaunchKernelGGL(k_match_rerank8, dim3((unsigned)(((int64_t)P * max_rows + 4 * kRrRows - 1) / (4 * kRrRows))),
                          dim3(256), 0, st, desc, count, cap, pairs, P, ratio, max_rows, cand, cand_n, cand_thr, rows);
     else if (abl == 0)
