@@ -101,7 +101,7 @@ def main():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=2,
+    ap.add_argument("--cpu-sample", type=int, default=8,
                     help="frames per host thread in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="disable the live per-stage HIP events")
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",

@@ -9,6 +9,8 @@
 // fma chain in row-major tap order (OpenCV FilterVec_32f's v_muladd chain; DESIGN.md
 // §Numerics).
 // VALU-bound by design.
+#include <stdlib.h>
+
 #include <algorithm>
 #include <utility>
 
@@ -393,7 +395,17 @@ void launch_harris(const float* lvl, float* R, uint32_t* hist, int B, int H, int
     case 4: launch_ks<4>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
     case 5: launch_ks<5>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
     case 6: launch_ks<6>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
-    case 7: launch_ks<7>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 7: {
+      // SFMFEAT_HARRIS_ABL=1|2: timing ablations inside the pipeline (results are wrong)
+      static const int abl = [] {
+        const char* e = getenv("SFMFEAT_HARRIS_ABL");
+        return e ? atoi(e) : 0;
+      }();
+      if (abl == 1) launch_ks<7, 1>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st);
+      else if (abl == 2) launch_ks<7, 2>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st);
+      else launch_ks<7>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st);
+      break;
+    }
     case 8: launch_ks<8>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
     case 9: launch_ks<9>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
     case 11: launch_ks<11>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
