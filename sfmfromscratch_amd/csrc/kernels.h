@@ -212,7 +212,7 @@ void launch_match_rows(const float* descT, const int32_t* count, int64_t capP, c
                        int P, float ratio, RowBest* rows, int max_rows, hipStream_t st);
 void launch_match_compact(const RowBest* rows, const int32_t* count, const int32_t* pairs, int P,
                           int max_rows, int64_t cap, int32_t* matches, float* conf, int32_t* nmatch,
-                          hipStream_t st);
+                          int* reset_counter, hipStream_t st);
 void init_match_attributes(int max_rows);
 // match_mfma.hip: exact matching with the split-fp16 MFMA prefilter
 void launch_match_prep(const float* desc, const int32_t* count, int nimg, int64_t cap, int64_t capP,

@@ -180,8 +180,12 @@ __global__ void __launch_bounds__(1024) k_match_compact(const RowBest* __restric
                                                         int max_rows, int64_t cap,
                                                         int32_t* __restrict__ matches,
                                                         float* __restrict__ conf,
-                                                        int32_t* __restrict__ nmatch) {
+                                                        int32_t* __restrict__ nmatch,
+                                                        int* __restrict__ reset_counter) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
+  // the MFMA matcher's overflow counter, read by k_match_overflow just before this kernel:
+  // zeroed here for the next call (no separate memset launch on the stream)
+  if (reset_counter != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *reset_counter = 0;
   uint64_t* s_k = reinterpret_cast<uint64_t*>(s_raw);
   __shared__ uint32_t s_n;
   const int p = blockIdx.x;
@@ -240,9 +244,9 @@ void launch_match_rows(const float* descT, const int32_t* count, int64_t capP, c
 
 void launch_match_compact(const RowBest* rows, const int32_t* count, const int32_t* pairs, int P,
                           int max_rows, int64_t cap, int32_t* matches, float* conf, int32_t* nmatch,
-                          hipStream_t st) {
+                          int* reset_counter, hipStream_t st) {
   hipLaunchKernelGGL(k_match_compact, dim3(P), dim3(1024), match_compact_lds(max_rows), st, rows, count,
-                     pairs, max_rows, cap, matches, conf, nmatch);
+                     pairs, max_rows, cap, matches, conf, nmatch, reset_counter);
 }
 
 }  // namespace sfm

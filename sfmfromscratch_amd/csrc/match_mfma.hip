@@ -686,7 +686,7 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
   }();
   const int qb = (max_rows + kQB - 1) / kQB;
   const dim3 grid((unsigned)(8 * ((P + 7) / 8) * qb));
-  (void)hipMemsetAsync(ovf_count, 0, sizeof(int), st);
+  // ovf_count is zero here: set once at allocation, re-zeroed by k_match_compact
 #define SFM_SWEEP(A)                                                                                           \
   hipLaunchKernelGGL(k_match_mfma<A>, grid, dim3(256), 0, st, count, capP, hi, lo, norm2, rnorm, imgmax, pairs, P, \
                      max_rows, cand, cand_n, cand_thr, ovf_count, ovf_list)

@@ -420,7 +420,10 @@ int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, in
   }
   if ((rc = ensure(c, c->m_rows, (size_t)P * cap * sizeof(RowBest)))) return rc;
   if ((rc = ensure(c, c->m_ovf, (size_t)P * cap * sizeof(int2)))) return rc;
-  if ((rc = ensure(c, c->m_ovfc, 16))) return rc;
+  if (c->m_ovfc.bytes == 0) {  // the overflow counter starts at zero; k_match_compact re-zeroes it
+    if ((rc = ensure(c, c->m_ovfc, 16))) return rc;
+    HIPCHK(c, hipMemsetAsync(c->m_ovfc.p, 0, 16, st));
+  }
   if (!c->match_direct) {  // admitted-target lists of the MFMA sweep (kMatchCandCap per row)
     if ((rc = ensure(c, c->m_cand, (size_t)P * cap * kMatchCandCap * 4))) return rc;
     if ((rc = ensure(c, c->m_candn, (size_t)P * cap * 4))) return rc;
@@ -441,7 +444,7 @@ int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, in
   {
     StageScope sc(c, SFM_PROF_MATCH_POST, st);
     launch_match_compact(as<RowBest>(c->m_rows), count, pairs, P, (int)cap, cap, matches, conf, nmatch,
-                         st);
+                         c->match_direct ? nullptr : as<int>(c->m_ovfc), st);
   }
   HIPCHK(c, hipGetLastError());
   return SFM_OK;
