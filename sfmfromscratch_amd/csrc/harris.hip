@@ -377,7 +377,11 @@ static void launch_ks(const float* lvl, float* R, uint32_t* hist, int B, int H, 
   int ntiles = tiles_x * tiles_y;
   // 2 resident workgroups per CU over the whole batch; each loops over tiles so the
   // digit histogram is flushed once per workgroup instead of once per tile
-  int per_plane = std::max(1, std::min(ntiles, 512 / std::max(B, 1)));
+  static const int slots = [] {  // SFMFEAT_HARRIS_SLOTS: resident-workgroup budget (A/B timing)
+    const char* e = getenv("SFMFEAT_HARRIS_SLOTS");
+    return e ? std::max(1, atoi(e)) : 512;
+  }();
+  int per_plane = std::max(1, std::min(ntiles, slots / std::max(B, 1)));
   if ((W & 3) == 0)
     hipLaunchKernelGGL((k_harris<KS, true, ABL>), dim3(per_plane, B), dim3(256), 0, st, lvl, R, hist, H, W,
                        tiles_x, ntiles, gk, alpha, scan);
