@@ -60,11 +60,18 @@ __device__ __forceinline__ void pk_fma_bcast(f32x2& acc, f32x2 k, f32x2 v) {
 // ABL (timing builds only): 0 = full kernel, 1 = no digit histogram, 2 = window sums over
 // the first tap row only.
 template <int KS, bool VEC, int ABL = 0>
-__global__ void __launch_bounds__(256, 2) k_harris(const float* __restrict__ lvl, float* __restrict__ Rout,
-                                                   uint32_t* __restrict__ hist_g, int H, int W,
-                                                   int tiles_x, int ntiles,
-                                                   const float* __restrict__ gk, float alpha,
-                                                   SelectScan scan) {
+__global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float* __restrict__ gk, float alpha) {
+  // this workgroup's level (one launch may hold several pyramid levels: the small levels'
+  // tiles share a launch instead of each paying a launch and a tail)
+  int li = 0;
+#pragma unroll
+  for (int k = 1; k < kHarrisMaxLevels; ++k) li += (k < lvs.n && (int)blockIdx.x >= lvs.l[k].wg0) ? 1 : 0;
+  const float* __restrict__ lvl = lvs.l[li].lvl;
+  float* __restrict__ Rout = lvs.l[li].R;
+  uint32_t* __restrict__ hist_g = lvs.l[li].hist;
+  const int H = lvs.l[li].H, W = lvs.l[li].W, tiles_x = lvs.l[li].tiles_x, ntiles = lvs.l[li].ntiles;
+  const SelectScan scan = lvs.l[li].scan;
+  const int wgx = (int)blockIdx.x - lvs.l[li].wg0, nwg = lvs.l[li].nwg;  // workgroups of this level's plane
   constexpr int GA = KS / 2;
   constexpr int PH = kHT + KS - 1;          // gradient rows of a tile (window halo)
   constexpr int NV = 4 + KS - 1;            // gradient values per row per thread
@@ -136,8 +143,8 @@ __global__ void __launch_bounds__(256, 2) k_harris(const float* __restrict__ lvl
       }
     }
   };
-  if (blockIdx.x < ntiles) prefetch(blockIdx.x);
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  if (wgx < ntiles) prefetch(wgx);
+  for (int tile = wgx; tile < ntiles; tile += nwg) {
     const int tx0 = (tile % tiles_x) * kHT;
     const int ty0 = (tile / tiles_x) * kHT;
     __syncthreads();  // the previous tile's LDS reads are done
@@ -155,7 +162,7 @@ __global__ void __launch_bounds__(256, 2) k_harris(const float* __restrict__ lvl
       }
     }
     __syncthreads();
-    if (tile + (int)gridDim.x < ntiles) prefetch(tile + gridDim.x);
+    if (tile + nwg < ntiles) prefetch(tile + nwg);
     // 1. gradients (NaiveSIFT.py:201-213: fma chain over the non-zero Sobel taps in
     //    row-major order from +0; k*p is exact for these taps) for 4-wide strips; outside
     //    the image the gradients are 0, so their products (:61-63) are the zero border of
@@ -362,61 +369,89 @@ __global__ void __launch_bounds__(256, 2) k_harris(const float* __restrict__ lvl
   // atomic loads.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) s_last = atomicAdd(&scan.done[(int64_t)b * kCounterStride], 1ull) == gridDim.x - 1 ? 1u : 0u;
+  if (tid == 0) s_last = atomicAdd(&scan.done[(int64_t)b * kCounterStride], 1ull) == (unsigned long long)(nwg - 1) ? 1u : 0u;
   __syncthreads();
   if (!s_last) return;
   select_scan_plane(hg, scan.state + b, scan.list_count + (int64_t)b * kCounterStride, (int64_t)H * W,
                     scan.vmin, scan.force_exact, s_red);
 }
 
-template <int KS, int ABL = 0>
-static void launch_ks(const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
-                      const float* gk, float alpha, SelectScan scan, hipStream_t st) {
-  int tiles_x = (W + kHT - 1) / kHT;
-  int tiles_y = (H + kHT - 1) / kHT;
-  int ntiles = tiles_x * tiles_y;
-  // 2 resident workgroups per CU over the whole batch; each loops over tiles so the
-  // digit histogram is flushed once per workgroup instead of once per tile
+// Workgroups per plane for a group of levels: a common tile budget per workgroup
+// T = ceil(sum of tiles / slots per plane), each level gets ceil(tiles / T) workgroups, so
+// every workgroup walks at most T tiles (2 resident per CU over the batch; each loops
+// over tiles so the digit histogram is flushed once per workgroup instead of once per tile)
+static int harris_plan(HarrisLevels& g, int B) {
   static const int slots = [] {  // SFMFEAT_HARRIS_SLOTS: resident-workgroup budget (A/B timing)
     const char* e = getenv("SFMFEAT_HARRIS_SLOTS");
     return e ? std::max(1, atoi(e)) : 512;
   }();
-  int per_plane = std::max(1, std::min(ntiles, slots / std::max(B, 1)));
-  if ((W & 3) == 0)
-    hipLaunchKernelGGL((k_harris<KS, true, ABL>), dim3(per_plane, B), dim3(256), 0, st, lvl, R, hist, H, W,
-                       tiles_x, ntiles, gk, alpha, scan);
-  else
-    hipLaunchKernelGGL((k_harris<KS, false, ABL>), dim3(per_plane, B), dim3(256), 0, st, lvl, R, hist, H, W,
-                       tiles_x, ntiles, gk, alpha, scan);
+  const int per_plane = std::max(1, slots / std::max(B, 1));
+  int total = 0;
+  for (int k = 0; k < g.n; ++k) total += g.l[k].ntiles;
+  const int T = std::max(1, (total + per_plane - 1) / per_plane);
+  int wg = 0;
+  for (int k = 0; k < g.n; ++k) {
+    g.l[k].wg0 = wg;
+    g.l[k].nwg = std::max(1, std::min(g.l[k].ntiles, (g.l[k].ntiles + T - 1) / T));
+    wg += g.l[k].nwg;
+  }
+  return wg;
 }
 
-void launch_harris(const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
-                   const float* d_gauss, int ks, float alpha, SelectScan scan, hipStream_t st) {
+template <int KS, int ABL = 0>
+static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipStream_t st) {
+  bool vec = true;
+  for (int k = 0; k < g.n; ++k) {
+    g.l[k].tiles_x = (g.l[k].W + kHT - 1) / kHT;
+    g.l[k].ntiles = g.l[k].tiles_x * ((g.l[k].H + kHT - 1) / kHT);
+    vec = vec && (g.l[k].W & 3) == 0;
+  }
+  const int nwg = harris_plan(g, B);
+  if (vec)
+    hipLaunchKernelGGL((k_harris<KS, true, ABL>), dim3(nwg, B), dim3(256), 0, st, g, gk, alpha);
+  else
+    hipLaunchKernelGGL((k_harris<KS, false, ABL>), dim3(nwg, B), dim3(256), 0, st, g, gk, alpha);
+}
+
+void launch_harris_levels(const HarrisLevels& g, int B, const float* d_gauss, int ks, float alpha, hipStream_t st) {
   switch (ks) {
-    case 1: launch_ks<1>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
-    case 2: launch_ks<2>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
-    case 3: launch_ks<3>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
-    case 4: launch_ks<4>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
-    case 5: launch_ks<5>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
-    case 6: launch_ks<6>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 1: launch_ks<1>(g, B, d_gauss, alpha, st); break;
+    case 2: launch_ks<2>(g, B, d_gauss, alpha, st); break;
+    case 3: launch_ks<3>(g, B, d_gauss, alpha, st); break;
+    case 4: launch_ks<4>(g, B, d_gauss, alpha, st); break;
+    case 5: launch_ks<5>(g, B, d_gauss, alpha, st); break;
+    case 6: launch_ks<6>(g, B, d_gauss, alpha, st); break;
     case 7: {
       // SFMFEAT_HARRIS_ABL=1|2: timing ablations inside the pipeline (results are wrong)
       static const int abl = [] {
         const char* e = getenv("SFMFEAT_HARRIS_ABL");
         return e ? atoi(e) : 0;
       }();
-      if (abl == 1) launch_ks<7, 1>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st);
-      else if (abl == 2) launch_ks<7, 2>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st);
-      else launch_ks<7>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st);
+      if (abl == 1) launch_ks<7, 1>(g, B, d_gauss, alpha, st);
+      else if (abl == 2) launch_ks<7, 2>(g, B, d_gauss, alpha, st);
+      else launch_ks<7>(g, B, d_gauss, alpha, st);
       break;
     }
-    case 8: launch_ks<8>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
-    case 9: launch_ks<9>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
-    case 11: launch_ks<11>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
-    case 13: launch_ks<13>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
-    case 15: launch_ks<15>(lvl, R, hist, B, H, W, d_gauss, alpha, scan, st); break;
+    case 8: launch_ks<8>(g, B, d_gauss, alpha, st); break;
+    case 9: launch_ks<9>(g, B, d_gauss, alpha, st); break;
+    case 11: launch_ks<11>(g, B, d_gauss, alpha, st); break;
+    case 13: launch_ks<13>(g, B, d_gauss, alpha, st); break;
+    case 15: launch_ks<15>(g, B, d_gauss, alpha, st); break;
     default: break;  // rejected at context creation
   }
+}
+
+void launch_harris(const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
+                   const float* d_gauss, int ks, float alpha, SelectScan scan, hipStream_t st) {
+  HarrisLevels g{};
+  g.n = 1;
+  g.l[0].lvl = lvl;
+  g.l[0].R = R;
+  g.l[0].hist = hist;
+  g.l[0].H = H;
+  g.l[0].W = W;
+  g.l[0].scan = scan;
+  launch_harris_levels(g, B, d_gauss, ks, alpha, st);
 }
 
 // Ablation timing (diagnostics): KS = 7 only, returns the mean launch time in ms.
@@ -425,12 +460,19 @@ float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, 
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
-  const SelectScan none{nullptr, nullptr, nullptr, 0, 0};
+  HarrisLevels g{};
+  g.n = 1;
+  g.l[0].lvl = lvl;
+  g.l[0].R = R;
+  g.l[0].hist = hist;
+  g.l[0].H = H;
+  g.l[0].W = W;
+  g.l[0].scan = SelectScan{nullptr, nullptr, nullptr, 0, 0};
   auto run = [&]() {
     switch (abl) {
-      case 1: launch_ks<7, 1>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
-      case 2: launch_ks<7, 2>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
-      default: launch_ks<7, 0>(lvl, R, hist, B, H, W, gk, alpha, none, 0); break;
+      case 1: launch_ks<7, 1>(g, B, gk, alpha, 0); break;
+      case 2: launch_ks<7, 2>(g, B, gk, alpha, 0); break;
+      default: launch_ks<7, 0>(g, B, gk, alpha, 0); break;
     }
   };
   run();

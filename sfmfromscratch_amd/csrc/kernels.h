@@ -161,6 +161,21 @@ void launch_resize(const float* src, int sh, int sw, float* dst, int dh, int dw,
 // scan.state set, the last workgroup of each plane also runs select_scan_plane.
 void launch_harris(const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
                    const float* d_gauss, int ks, float alpha, SelectScan scan, hipStream_t st);
+// Several pyramid levels of a batch in one Harris launch (workgroups partitioned by
+// level; tiles_x / ntiles / wg0 / nwg are filled in by the launcher)
+constexpr int kHarrisMaxLevels = 4;
+struct HarrisLevels {
+  struct Level {
+    const float* lvl;
+    float* R;
+    uint32_t* hist;
+    int H, W, tiles_x, ntiles, wg0, nwg;
+    SelectScan scan;
+  } l[kHarrisMaxLevels];
+  int n;
+};
+void launch_harris_levels(const HarrisLevels& g, int B, const float* d_gauss, int ks, float alpha,
+                          hipStream_t st);
 
 float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
                            const float* gk, float alpha, int iters);
