@@ -31,6 +31,7 @@ constexpr int kWaves = 4;              // waves per workgroup
 constexpr int kQB = kQW * kWaves;      // 128 query rows per workgroup
 constexpr int kRowH = 128 + 8;         // padded fp16 row in LDS (272 B): conflict-free b128 reads
 constexpr int kCandCap = kMatchCandCap;  // admitted targets per query row (global list)
+constexpr int kHalfCap = kCandCap / 2;   // each half-wave's share of a row's list
 constexpr float kScale = 256.0f;       // operand pre-scale (2^8)
 constexpr float kLoScale = 2048.0f;    // lo part scale (2^11)
 
@@ -132,6 +133,14 @@ SFM_DEV uint16_t bf16_down(float v) {
   return v >= 0.0f ? (uint16_t)(__float_as_uint(v) >> 16) : (uint16_t)0xFF80u;
 }
 
+// x of the lane 32 away (the other half of the wavefront): one v_permlane32_swap + a select,
+// instead of a ds_bpermute through the LDS crossbar
+SFM_DEV float other_half(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+}
+SFM_DEV int other_half(int x) { return __float_as_int(other_half(__int_as_float(x))); }
+
 SFM_DEV void top2_merge(float& b1, int& j1, float& b2, float ob1, int oj1, float ob2) {
   if (ob1 < b1 || (ob1 == b1 && oj1 < j1)) {
     b2 = fminf(b1, ob2);
@@ -153,14 +162,17 @@ constexpr int kStageHalves = kTT2 * kRowH;  // f16 elements per array per stage
 // (two v_med3) and admits the target when d~ <= thr, thr = b2~(so far) + 2E: this lane's
 // own b2~ after the sub-tile, capped by the wave-merged b2~ of the previous stage.  b2~
 // only decreases, so every running thr >= the final one and the admitted set contains
-// the row's final window (argument below).  Admitted target indices go to the row's list
-// in global memory (kCandCap entries); k_match_rerank recomputes them with the
-// reference's exact float32 distance; a row whose list overflowed goes to
-// k_match_overflow (exact over all targets).
+// the row's final window (argument below).  thr uses the row's b2~ over both half-waves
+// (merged after every sub-tile).  Admitted target indices go to the row's list in global
+// memory: each half-wave lane appends to its own kHalfCap entries with a register count
+// (no LDS atomics), and the row's count word holds both (low / high 16 bits);
+// k_match_rerank recomputes them with the reference's exact float32 distance; a row
+// whose list overflowed goes to k_match_overflow (exact over all targets).
 // The window argument: the targets achieving b1~ and b2~ have exact distances <= b1~ + E and
 // <= b2~ + E, so the exact second-smallest D2 <= b2~ + E; a target with exact d <= D2 has
 // d~ <= d + E <= b2~ + 2E.  Targets outside the window are strictly farther than D2.
-// ABL (timing builds only; results are wrong unless 0): 9 = no epilogue, 10 = no MFMAs
+// ABL (timing builds only; results are wrong unless 0): 9 = no epilogue, 10 = no MFMAs,
+// 11 = no stage loads (every stage reuses stage 0's LDS rows), 12 = no list appends
 template <int ABL>
 __global__ void __launch_bounds__(256, 2) k_match_mfma(
     const int32_t* __restrict__ count, int64_t capP, const _Float16* __restrict__ hi,
@@ -170,7 +182,6 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
     int* __restrict__ ovf_count, int2* __restrict__ ovf_list) {
   __shared__ __attribute__((aligned(16))) _Float16 sT[2][kStageHalves];
   __shared__ __attribute__((aligned(16))) float sN[2][kTT2];  // target norms, by stage parity
-  __shared__ int sCnt[kQB];
   __shared__ __attribute__((aligned(16))) float sD[kWaves][64][16];  // a sub-tile's d~ per lane
 
   // XCD-aware mapping (workgroups b and b + 8 share an XCD and its L2): group g = b % 8
@@ -204,9 +215,9 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
   // rigorous |d~ - d_ref| bound (matcher exactness)
   const float E = 3.0517578125e-05f * ra * maxrn + 4e-6f * (na + maxn2) + 1.25e-4f;
   const float E2 = 2.0f * E;
-  for (int i = tid; i < kQB; i += 256) sCnt[i] = 0;
   const bool live = qi < n1;
-  uint32_t* my_list = cand + ((int64_t)p * max_rows + qi) * kCandCap;
+  uint32_t* my_list = cand + ((int64_t)p * max_rows + qi) * kCandCap + half * kHalfCap;
+  int cnt = 0;  // this lane's appended targets (its half of the row)
 
   const int nst = (n2 + kTT2 - 1) / kTT2;
   const int64_t to = (int64_t)i2 * capP * 128;
@@ -216,6 +227,7 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
   const int lr = tid >> 4, lc = (tid & 15) * 8;
   h8 g[8];
   auto load_stage = [&](int st) {
+    if (ABL == 11 && st > 0) return;
     const int64_t gofs = to + (int64_t)(st * kTT2) * 128 + tid * 8;  // rows < capP: in bounds
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -223,7 +235,8 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
       g[4 + q] = *reinterpret_cast<const h8*>(lo + gofs + 2048 * q);
     }
   };
-  auto store_stage = [&]() {
+  auto store_stage = [&](bool first) {
+    if (ABL == 11 && !first) return;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       *reinterpret_cast<h8*>(&sT[0][(16 * q + lr) * kRowH + lc]) = g[q];
@@ -277,7 +290,9 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
       b2 = __builtin_amdgcn_fmed3f(b1, b2, d[rr]);
       b1 = __builtin_amdgcn_fmed3f(b1, d[rr], -INFINITY);
     }
-    const float t = fminf(b2 + E2, thr_w);
+    // the row's b2~ so far over both halves (every lane's b2 and b1 >= its half's final ones)
+    const float ob1 = other_half(b1), ob2 = other_half(b2);
+    const float t = fminf(fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + E2, thr_w);
 #pragma unroll
     for (int rr = 0; rr < 16; ++rr) mm |= (d[rr] <= t) ? (1u << rr) : 0u;
   };
@@ -307,16 +322,19 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
   // each admitted one is read back by index (no dynamic register indexing into d)
   float* my_d = &sD[wid][lane][0];
   auto append = [&](uint32_t mm, const float (&d)[16], int jb) {
+    if (ABL == 12) {
+      asm volatile("" ::"v"(mm));
+      return;
+    }
     if (__any(mm != 0u)) {  // wave-uniform: skip when no lane admits
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         *reinterpret_cast<float4*>(my_d + 4 * q) = make_float4(d[4 * q], d[4 * q + 1], d[4 * q + 2], d[4 * q + 3]);
-      if (live && mm) {  // reserve this lane's slots with one LDS atomic, then fill them
-        int slot = atomicAdd(&sCnt[ql], __popc(mm));
-        for (; mm; mm &= mm - 1, ++slot) {
+      if (live && mm) {
+        for (; mm; mm &= mm - 1, ++cnt) {
           const int rr = __builtin_ctz(mm);
-          if (slot < kCandCap)
-            my_list[slot] = (uint32_t)(jb + 4 * half + (rr & 3) + 8 * (rr >> 2)) | ((uint32_t)bf16_down(my_d[rr]) << 16);
+          if (cnt < kHalfCap)
+            my_list[cnt] = (uint32_t)(jb + 4 * half + (rr & 3) + 8 * (rr >> 2)) | ((uint32_t)bf16_down(my_d[rr]) << 16);
         }
       }
     }
@@ -324,7 +342,7 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
 
   load_stage(0);
   const float nrm_t0 = (tid < kTT2) ? norm2[(int64_t)i2 * capP + tid] : 0.0f;
-  store_stage();
+  store_stage(true);
   if (tid < kTT2) {
     sN[0][tid] = nrm_t0;
     sN[1][tid] = INFINITY;  // "stage -1": the carried sub-tile's first epilogue is a no-op
@@ -365,11 +383,11 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
       ph_x = x1;
     }
     {  // the wave-merged running threshold for the next stage (both halves of a row)
-      const float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
+      const float ob1 = other_half(b1), ob2 = other_half(b2);
       thr_w = fminf(fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + E2, thr_w);
     }
     __syncthreads();  // every wave is done with this stage's LDS rows and norms
-    store_stage();
+    store_stage(false);
     if (tid < kTT2) sN[par ^ 1][tid] = nrm_next;
   }
   {
@@ -381,20 +399,19 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
   }
   // the row's final window threshold (both halves merged): the re-rank drops the admitted
   // targets above it (their stored d~ is rounded down, so no window member is dropped)
-  const float ob1 = __shfl_xor(b1, 32), ob2 = __shfl_xor(b2, 32);
+  const float ob1 = other_half(b1), ob2 = other_half(b2);
   const float thr_final = fminf(fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + E2, thr_w);
   if (ABL != 0) {
     if (thr_final == -1.0f) cand_n[0] = 1;  // defeats dead-code elimination
     return;
   }
-  if (live && half == 0) cand_thr[(int64_t)p * max_rows + qi] = thr_final;
-  __syncthreads();
-  if (tid < kQB && row0 + tid < n1) {
-    const int c = sCnt[tid];
-    cand_n[(int64_t)p * max_rows + row0 + tid] = c;
-    if (c > kCandCap) {  // the list overflowed: exact over every target instead
+  const int ocnt = other_half(cnt);
+  if (live && half == 0) {
+    cand_thr[(int64_t)p * max_rows + qi] = thr_final;
+    cand_n[(int64_t)p * max_rows + qi] = cnt | (ocnt << 16);  // n2 < 2^16 (kMaxMatchRows)
+    if (cnt > kHalfCap || ocnt > kHalfCap) {  // a list overflowed: exact over every target instead
       const int k = atomicAdd(ovf_count, 1);
-      ovf_list[k] = make_int2(p, row0 + tid);
+      ovf_list[k] = make_int2(p, qi);
     }
   }
 }
@@ -424,8 +441,9 @@ __global__ void __launch_bounds__(256) k_match_rerank(const float* __restrict__ 
   const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
   const int n1 = count[i1], n2 = count[i2];
   if (row >= n1 || n2 < 1) return;
-  const int c = cand_n[w];
-  if (c > kCandCap) return;  // k_match_overflow's row
+  const int cw = cand_n[w];
+  const int c0 = cw & 0xffff, c1 = cw >> 16;  // the two half-lists' lengths
+  if (c0 > kHalfCap || c1 > kHalfCap) return;  // k_match_overflow's row
   const float thr = cand_thr[w];
   const uint32_t* list = cand + w * kCandCap;
   const float* A = desc + ((int64_t)i1 * cap + row) * 128;
@@ -434,10 +452,14 @@ __global__ void __launch_bounds__(256) k_match_rerank(const float* __restrict__ 
 #pragma unroll
   for (int i = 0; i < 16; ++i) a[i] = A[8 * i + l8];
   int nk = 0;  // window members, compacted into sJ[wv] in list order
-  for (int s0 = 0; s0 < c; s0 += 64) {
-    const int s = s0 + lane;
-    const uint32_t e = s < c ? list[s] : 0u;
-    const bool keep = s < c && __uint_as_float(e & 0xffff0000u) <= thr;
+  static_assert(kHalfCap == 64, "one wavefront pass per half-list");
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int ch = h ? c1 : c0;
+    if (ch == 0) continue;
+    const bool in = lane < ch;
+    const uint32_t e = in ? list[h * kHalfCap + lane] : 0u;
+    const bool keep = in && __uint_as_float(e & 0xffff0000u) <= thr;
     const uint64_t bal = __ballot(keep);
     if (keep) sJ[wv][nk + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(e & 0xffffu);
     nk += __popcll(bal);
@@ -533,9 +555,9 @@ __global__ void __launch_bounds__(256) k_match_rerank8(const float* __restrict__
       i2_l = pairs[2 * p_l + 1];
       const int n1 = count[i1_l], n2 = count[i2_l];
       if (row_l < n1 && n2 >= 1) {
-        c_l = cand_n[w];
+        c_l = cand_n[w];  // half-list lengths, low / high 16 bits
         thr_l = cand_thr[w];
-        ok_l = c_l <= kCandCap ? 1 : 0;  // overflowed rows belong to k_match_overflow
+        ok_l = ((c_l & 0xffff) <= kHalfCap && (c_l >> 16) <= kHalfCap) ? 1 : 0;  // else k_match_overflow's row
       }
     }
     if (!ok_l) c_l = 0;
@@ -559,7 +581,8 @@ __global__ void __launch_bounds__(256) k_match_rerank8(const float* __restrict__
     const int r = e / kCandCap, pos = e % kCandCap;  // r is wave-uniform per sidx
     const int cr = __shfl(c_l, r);
     const float tr = __shfl(thr_l, r);
-    const bool valid = pos < cr && w0 + r < total;
+    const int crh = pos < kHalfCap ? (cr & 0xffff) : (cr >> 16);
+    const bool valid = (pos & (kHalfCap - 1)) < crh && w0 + r < total;
     const uint32_t ent = valid ? lists[e] : 0u;
     const bool keep = valid && __uint_as_float(ent & 0xffff0000u) <= tr;
     const uint64_t bal = __ballot(keep);
@@ -694,6 +717,10 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
     SFM_SWEEP(9);
   else if (abl == 10)
     SFM_SWEEP(10);
+  else if (abl == 11)
+    SFM_SWEEP(11);
+  else if (abl == 12)
+    SFM_SWEEP(12);
   else
     SFM_SWEEP(0);
 #undef SFM_SWEEP
