@@ -18,6 +18,8 @@
 // loads into registers one tile ahead, then staged through LDS.  HBM-bound: ~1.03 reads
 // of R (the column halo's lines are the neighbour tiles', fetched by the same workgroup).
 // k_nms_generic (larger ksize): separable window max on an LDS tile.
+#include <stdlib.h>
+
 #include <algorithm>
 #include <type_traits>
 
@@ -267,7 +269,12 @@ static void launch_tile(const float* R, const MedianState* state, uint64_t* cand
   const int ntiles = tiles_x * ((H + kTT_H - 1) / kTT_H);
   // contiguous row-major tile ranges per workgroup (enough workgroups to keep the bytes in
   // flight: each holds one tile of prefetch)
-  dim3 grid(std::min(ntiles, kNmsBlocksPerPlane), B);
+  static const int slots = [] {  // SFMFEAT_NMS_SLOTS: workgroups per launch over all planes (A/B)
+    const char* e = getenv("SFMFEAT_NMS_SLOTS");
+    return e ? atoi(e) : 0;
+  }();
+  const int per_plane = slots > 0 ? std::max(1, slots / std::max(B, 1)) : kNmsBlocksPerPlane;
+  dim3 grid(std::min(ntiles, per_plane), B);
   const bool vec = (W & 3) == 0;
   if (mode == 0 && vec)
     hipLaunchKernelGGL((k_nms_tile<KH, 0, true>), grid, dim3(256), 0, st, R, state, cand, cnt, H, W, tiles_x, ntiles);
