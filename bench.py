@@ -51,7 +51,7 @@ HARRIS_FLOP_PER_PX = 328   # Sobel 2x6 fma (24) + 3 products + 3x49 fma (294) + 
 MATCH_FLOP_PER_ELEM = 2    # GEMM-equivalent: one multiply-add per descriptor element pair
 DESC_BYTES_PER_KP = 20 * 20 * 4 + 128 * 4 + 12   # level window + halo read, descriptor + xy/conf written
 KERNELS = {"harris": "k_harris<7>", "match": "k_match_mfma", "describe": "k_describe_q",
-           "nms": "k_nms_tile<1,0,true>", "median": "k_med_scan", "topk": "k_topk", "pyramid": "k_down2x3",
+           "nms": "k_nms_stream<8,256>", "median": "k_med_scan", "topk": "k_topk", "pyramid": "k_down2x3",
            "match_prep": "k_match_prep", "match_post": "k_match_compact"}
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")  # tools/pmc_traffic.py
 

@@ -261,6 +261,12 @@ int32_t sfm_debug_harris(int32_t device, const float* gauss, int32_t gs, double 
                          int32_t ksize, const float* img, int32_t H, int32_t W, float* R_out,
                          float* median_out, int64_t* ncand_out);
 
+/* Certified-mode NMS candidates (NaiveSIFT.py:77-95 with keys >= tnms[b]) of B planes:
+ * unordered u64 keys ~fkey(R) << 32 | raster index in keys_out[b*H*W ...], counts_out[b] of
+ * them.  tile = 1 forces the tiled kernel where the streaming one runs by default. */
+int32_t sfm_debug_nms(int32_t device, const float* R, int32_t B, int32_t H, int32_t W, int32_t ksize,
+                      const uint32_t* tnms, int32_t tile, uint64_t* keys_out, int64_t* counts_out);
+
 /* Mean time (ms) of one fused Harris launch on synthetic planes, ablation variant abl
  * (0 full, 1 no digit histogram, 2 window sums over the first tap row only). */
 float sfm_debug_time_harris(int32_t device, int32_t abl, int32_t B, int32_t H, int32_t W,

@@ -69,6 +69,8 @@ SIGNATURES = {
     "sfm_debug_atan2": (ctypes.c_int32, [ctypes.c_int32, _fp, _fp, _fp, ctypes.c_int64]),
     "sfm_debug_harris": (ctypes.c_int32, [ctypes.c_int32, _fp, ctypes.c_int32, ctypes.c_double, ctypes.c_int32,
                                           _fp, ctypes.c_int32, ctypes.c_int32, _fp, _fp, _i64p]),
+    "sfm_debug_nms": (ctypes.c_int32, [ctypes.c_int32, _fp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_int32, _vp, ctypes.c_int32, _vp, _i64p]),
 }
 
 
@@ -321,6 +323,19 @@ def debug_harris(img: np.ndarray, params: SfmParams, device: int = 0):
                                           img.ctypes.data_as(_fp), H, W, R.ctypes.data_as(_fp),
                                           med.ctypes.data_as(_fp), ctypes.byref(nc)))
     return R, med[0], nc.value
+
+
+def debug_nms(R: np.ndarray, tnms, ksize: int = 3, tile: bool = False, device: int = 0):
+    """Certified-mode NMS of B planes R [B, H, W] f32 with per-plane key thresholds tnms [B]
+    -> list of B sorted uint64 key arrays (~fkey(R) << 32 | raster index)."""
+    R = np.ascontiguousarray(R, dtype=np.float32)
+    B, H, W = R.shape
+    t = np.ascontiguousarray(tnms, dtype=np.uint32)
+    keys = np.zeros(B * H * W, np.uint64)
+    cnt = np.zeros(B, np.int64)
+    check(load_library().sfm_debug_nms(device, R.ctypes.data_as(_fp), B, H, W, ksize, t.ctypes.data,
+                                       int(tile), keys.ctypes.data, cnt.ctypes.data_as(_i64p)))
+    return [np.sort(keys[b * H * W: b * H * W + cnt[b]]) for b in range(B)]
 
 
 _tls = threading.local()

@@ -86,6 +86,44 @@ int32_t sfm_debug_harris(int32_t device, const float* gauss, int32_t gs, double 
   return rc;
 }
 
+// Certified-mode NMS (the predicate of NaiveSIFT.py:77-95 restricted to keys >= tnms, §5)
+// on B host planes with per-plane thresholds tnms[B]: the candidate keys of plane b land in
+// keys_out[b * H * W ...] (unordered), their number in counts_out[b].  tile = 1 runs the
+// tiled kernel where the streaming one would run, so the tests can hold both to one oracle.
+int32_t sfm_debug_nms(int32_t device, const float* R, int32_t B, int32_t H, int32_t W, int32_t ksize,
+                      const uint32_t* tnms, int32_t tile, uint64_t* keys_out, int64_t* counts_out) {
+  if (B < 1 || H < 1 || W < 1 || ksize < 1 || (ksize & 1) == 0 || ksize / 2 > SFM_NMS_MAX_HALF) return SFM_EINVAL;
+  if (hipSetDevice(device) != hipSuccess) return SFM_EDEVICE;
+  const int64_t n = (int64_t)H * W, tot = n * B;
+  float* d_R = nullptr;
+  MedianState* d_med = nullptr;
+  unsigned long long* d_cnt = nullptr;
+  uint64_t* d_cand = nullptr;
+  int32_t rc = SFM_OK;
+  if (hipMalloc(&d_R, tot * 4) || hipMalloc(&d_med, sizeof(MedianState) * B) ||
+      hipMalloc(&d_cnt, 8 * (size_t)B * kCounterStride) || hipMalloc(&d_cand, tot * 8)) {
+    rc = SFM_EDEVICE;
+  } else {
+    std::vector<MedianState> ms(B);
+    memset(ms.data(), 0, sizeof(MedianState) * B);
+    for (int b = 0; b < B; ++b) ms[b].tnms = tnms[b];  // fallback = 0: certified planes
+    (void)hipMemcpy(d_R, R, tot * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_med, ms.data(), sizeof(MedianState) * B, hipMemcpyHostToDevice);
+    (void)hipMemset(d_cnt, 0, 8 * (size_t)B * kCounterStride);
+    launch_nms(d_R, d_med, d_cand, d_cnt, B, H, W, ksize, 0, 0, tile);
+    std::vector<unsigned long long> cnt((size_t)B * kCounterStride);
+    if (hipDeviceSynchronize() || hipMemcpy(cnt.data(), d_cnt, 8 * cnt.size(), hipMemcpyDeviceToHost) ||
+        hipMemcpy(keys_out, d_cand, tot * 8, hipMemcpyDeviceToHost)) {
+      rc = SFM_EDEVICE;
+    } else {
+      for (int b = 0; b < B; ++b) counts_out[b] = (int64_t)cnt[(size_t)b * kCounterStride];
+    }
+  }
+  void* bufs[] = {d_R, d_med, d_cnt, d_cand};
+  for (void* b : bufs) (void)hipFree(b);
+  return rc;
+}
+
 // Mean time (ms) of one k_harris<7> launch over B x H x W synthetic planes for ablation
 // variant `abl` (0 full, 1 no histogram, 2 no window sums, 3 no Sobel/products).
 float sfm_debug_time_harris(int32_t device, int32_t abl, int32_t B, int32_t H, int32_t W, int32_t iters) {

@@ -191,8 +191,10 @@ void launch_median_exact(const float* R, MedianState* state, uint32_t* list, uns
 // nms.hip: candidates as 64-bit keys (~fkey(conf) << 32 | raster index), appended per
 // plane.  mode 0 (certified planes): R == window max && key(R) >= tnms; mode 1 (fallback
 // planes): the exact predicate (R == window max, or R == 0 below the median).
+// force_tile: the tiled kernel for the certified 3x3 case too (parity test of both forms)
 void launch_nms(const float* R, const MedianState* state, uint64_t* cand,
-                unsigned long long* cand_count, int B, int H, int W, int ksize, int mode, hipStream_t st);
+                unsigned long long* cand_count, int B, int H, int W, int ksize, int mode, hipStream_t st,
+                int force_tile = 0);
 
 // select.hip: top-k by (conf desc, index asc) + edge filter (NaiveSIFT.py:99-120).
 void init_topk_attributes();

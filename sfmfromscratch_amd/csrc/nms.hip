@@ -199,9 +199,9 @@ __global__ void __launch_bounds__(256) k_nms_tile(const float* __restrict__ R,
 // (plus the strip's two halo rows).  All SH + 2 rows are loaded up front (16-B loads, one
 // per row), the horizontal max3 takes its outer columns from the neighbouring lanes
 // (__shfl_up/__shfl_down; the wave's edge lanes load them), then the vertical max3 and the
-// predicate.  No LDS staging and no barriers: the tiled kernel's per-tile barriers and
-// LDS round trip paced it at ~21 % of HBM.  Candidates are appended with
-// one atomic per wavefront; their order is irrelevant (k_topk orders them by key).
+// predicate.  No LDS staging: the tiled kernel's per-tile barriers and LDS round trip
+// paced it at ~21 % of HBM.  Candidates are appended with one atomic per
+// workgroup; their order is irrelevant (k_topk orders them by key).
 template <int SH, int NT>
 __global__ void __launch_bounds__(NT) k_nms_stream(const float* __restrict__ R,
                                                     const MedianState* __restrict__ st,
@@ -217,84 +217,89 @@ __global__ void __launch_bounds__(NT) k_nms_stream(const float* __restrict__ R,
   const float* Rp = R + (int64_t)b * n;
   const int C4 = W >> 2;
   const int lane = threadIdx.x & 63;
-  const int64_t gid = (int64_t)blockIdx.x * NT + threadIdx.x;
-  const bool active = gid < (int64_t)C4 * nstrips;
-  const int g = active ? (int)gid : C4 * nstrips - 1;  // inactive lanes mirror the last group
-  const int s = g / C4, c4 = g - s * C4;
-  const int y0 = s * SH - 1;  // buffer row j is image row y0 + j
-  const float* colp = Rp + 4 * c4;
-
-  float4 v[NR];
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    const int gy = min(max(y0 + j, 0), H - 1);
-    v[j] = *reinterpret_cast<const float4*>(colp + (int64_t)gy * W);
-  }
-  // the wave's edge lanes fetch the column beyond their group (the neighbour lane's value
-  // is in another wavefront); the same 128-B lines are being read by that wavefront
-  float edge[NR];
-  const bool need_l = lane == 0 && c4 > 0, need_r = lane == 63 && c4 < C4 - 1;
-#pragma unroll
-  for (int j = 0; j < NR; ++j) edge[j] = -INFINITY;
-  if (need_l || need_r) {
-    const int off = need_l ? -1 : 4;
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const int gy = min(max(y0 + j, 0), H - 1);
-      edge[j] = colp[(int64_t)gy * W + off];
-    }
-  }
-
-  // rolling horizontal maxima: hm[j % 3] holds buffer row j; output row i = buffer row
-  // i + 1 is decided once buffer row i + 2 is in
-  float hm[3][4];
-  uint64_t flags = 0;
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    const bool rowok = y0 + j >= 0 && y0 + j < H;
-    if (!rowok) v[j] = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-    const float up = __shfl_up(v[j].w, 1);    // lane - 1's last column
-    const float dn = __shfl_down(v[j].x, 1);  // lane + 1's first column
-    float l = c4 == 0 ? -INFINITY : (lane == 0 ? edge[j] : up);
-    float r = c4 == C4 - 1 ? -INFINITY : (lane == 63 ? edge[j] : dn);
-    if (!rowok) l = r = -INFINITY;
-    float* h = hm[j % 3];
-    h[0] = fmaxf(fmaxf(l, v[j].x), v[j].y);
-    h[1] = fmaxf(fmaxf(v[j].x, v[j].y), v[j].z);
-    h[2] = fmaxf(fmaxf(v[j].y, v[j].z), v[j].w);
-    h[3] = fmaxf(fmaxf(v[j].z, v[j].w), r);
-    if (j >= 2) {
-      const int i = j - 2;
-      const float c[4] = {v[i + 1].x, v[i + 1].y, v[i + 1].z, v[i + 1].w};
-      const bool inside = active && !dry && y0 + 1 + i < H;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float m = fmaxf(fmaxf(hm[0][e], hm[1][e]), hm[2][e]);
-        const bool pred = inside && fkey(c[e]) >= tnms && c[e] == m;
-        flags |= pred ? (1ull << (4 * i + e)) : 0ull;
-      }
-    }
-  }
-
-  // one atomic per workgroup (device-scope atomics on the per-plane counters, not the
-  // bytes, paced the per-wavefront form: a candidate-free pass over R took 58 us at L0
-  // against 93 us with the appends)
+  // persistent workgroups (the grid may be capped, SFMFEAT_NMS_STREAM_WG): virtual block vb
+  // covers groups [vb * NT, vb * NT + NT); every thread of a workgroup runs the same vb's
   __shared__ uint32_t s_wsum[NT / 64];
   __shared__ unsigned long long s_base;
-  if (!__syncthreads_or(flags != 0)) return;
-  const int64_t slot = block_append(&cand_count[(int64_t)b * kCounterStride], (uint32_t)__popcll(flags),
-                                    s_wsum, &s_base);
-  if (flags == 0) return;
-  uint64_t* out = cand + (int64_t)b * n + slot;
-#pragma unroll
-  for (int i = 0; i < SH; ++i) {
-    if ((flags >> (4 * i)) & 0xFull) {
-      const float c[4] = {v[i + 1].x, v[i + 1].y, v[i + 1].z, v[i + 1].w};
-      const uint32_t rowidx = (uint32_t)((y0 + 1 + i) * W + 4 * c4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if ((flags >> (4 * i + e)) & 1ull) *out++ = ((uint64_t)(~fkey(c[e])) << 32) | (rowidx + e);
+  const int64_t nvb = ((int64_t)C4 * nstrips + NT - 1) / NT;
+  for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+    const int64_t gid = vb * NT + threadIdx.x;
+    const bool active = gid < (int64_t)C4 * nstrips;
+    const int g = active ? (int)gid : C4 * nstrips - 1;  // inactive lanes mirror the last group
+    const int s = g / C4, c4 = g - s * C4;
+    const int y0 = s * SH - 1;  // buffer row j is image row y0 + j
+    const float* colp = Rp + 4 * c4;
+
+    float4 v[NR];
+  #pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int gy = min(max(y0 + j, 0), H - 1);
+      v[j] = *reinterpret_cast<const float4*>(colp + (int64_t)gy * W);
     }
+    // the wave's edge lanes fetch the column beyond their group (the neighbour lane's value
+    // is in another wavefront); the same 128-B lines are being read by that wavefront
+    float edge[NR];
+    const bool need_l = lane == 0 && c4 > 0, need_r = lane == 63 && c4 < C4 - 1;
+  #pragma unroll
+    for (int j = 0; j < NR; ++j) edge[j] = -INFINITY;
+    if (need_l || need_r) {
+      const int off = need_l ? -1 : 4;
+  #pragma unroll
+      for (int j = 0; j < NR; ++j) {
+        const int gy = min(max(y0 + j, 0), H - 1);
+        edge[j] = colp[(int64_t)gy * W + off];
+      }
+    }
+
+    // rolling horizontal maxima: hm[j % 3] holds buffer row j; output row i = buffer row
+    // i + 1 is decided once buffer row i + 2 is in
+    float hm[3][4];
+    uint64_t flags = 0;
+  #pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const bool rowok = y0 + j >= 0 && y0 + j < H;
+      if (!rowok) v[j] = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      const float up = __shfl_up(v[j].w, 1);    // lane - 1's last column
+      const float dn = __shfl_down(v[j].x, 1);  // lane + 1's first column
+      float l = c4 == 0 ? -INFINITY : (lane == 0 ? edge[j] : up);
+      float r = c4 == C4 - 1 ? -INFINITY : (lane == 63 ? edge[j] : dn);
+      if (!rowok) l = r = -INFINITY;
+      float* h = hm[j % 3];
+      h[0] = fmaxf(fmaxf(l, v[j].x), v[j].y);
+      h[1] = fmaxf(fmaxf(v[j].x, v[j].y), v[j].z);
+      h[2] = fmaxf(fmaxf(v[j].y, v[j].z), v[j].w);
+      h[3] = fmaxf(fmaxf(v[j].z, v[j].w), r);
+      if (j >= 2) {
+        const int i = j - 2;
+        const float c[4] = {v[i + 1].x, v[i + 1].y, v[i + 1].z, v[i + 1].w};
+        const bool inside = active && !dry && y0 + 1 + i < H;
+  #pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float m = fmaxf(fmaxf(hm[0][e], hm[1][e]), hm[2][e]);
+          const bool pred = inside && fkey(c[e]) >= tnms && c[e] == m;
+          flags |= pred ? (1ull << (4 * i + e)) : 0ull;
+        }
+      }
+    }
+
+    // one atomic per workgroup (device-scope atomics on the per-plane counters, not the
+    // bytes, paced the per-wavefront form: a candidate-free pass over R took 58 us at L0
+    // against 93 us with the appends)
+    if (!__syncthreads_or(flags != 0)) continue;
+    const int64_t slot = block_append(&cand_count[(int64_t)b * kCounterStride], (uint32_t)__popcll(flags),
+                                      s_wsum, &s_base);
+    if (flags == 0) continue;
+    uint64_t* out = cand + (int64_t)b * n + slot;
+  #pragma unroll
+    for (int i = 0; i < SH; ++i) {
+      if ((flags >> (4 * i)) & 0xFull) {
+        const float c[4] = {v[i + 1].x, v[i + 1].y, v[i + 1].z, v[i + 1].w};
+        const uint32_t rowidx = (uint32_t)((y0 + 1 + i) * W + 4 * c4);
+  #pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if ((flags >> (4 * i + e)) & 1ull) *out++ = ((uint64_t)(~fkey(c[e])) << 32) | (rowidx + e);
+  }
+}
   }
 }
 
@@ -380,9 +385,9 @@ __global__ void __launch_bounds__(256) k_nms_generic(const float* __restrict__ R
 
 template <int KH>
 static void launch_tile(const float* R, const MedianState* state, uint64_t* cand, unsigned long long* cnt,
-                        int B, int H, int W, int tiles_x, int mode, hipStream_t st) {
+                        int B, int H, int W, int tiles_x, int mode, hipStream_t st, int force_tile) {
   const bool vec = (W & 3) == 0;
-  if (KH == 1 && mode == 0 && vec && !nms_tile_forced()) {
+  if (KH == 1 && mode == 0 && vec && !force_tile && !nms_tile_forced()) {
     // SFMFEAT_NMS_SH=8: 8-row strips (A/B); SFMFEAT_NMS_DRY=1: a candidate-free read pass
     // of R ahead of the real one (timing only: how fast R reads once Harris's writes drained)
     static const int sh = [] { const char* e = getenv("SFMFEAT_NMS_SH"); return e ? atoi(e) : kStreamSH; }();
@@ -391,7 +396,10 @@ static void launch_tile(const float* R, const MedianState* state, uint64_t* cand
     const int NTr = 256;
     const int nstrips = (H + SHr - 1) / SHr;
     const int64_t threads = (int64_t)(W >> 2) * nstrips;
-    dim3 grid((unsigned)((threads + NTr - 1) / NTr), B);
+    static const int wg = [] { const char* e = getenv("SFMFEAT_NMS_STREAM_WG"); return e ? atoi(e) : 0; }();
+    const int64_t nvb = (threads + NTr - 1) / NTr;
+    // SFMFEAT_NMS_STREAM_WG=n: at most n workgroups per launch over all planes (persistent)
+    dim3 grid((unsigned)(wg > 0 ? std::min<int64_t>(nvb, std::max(1, wg / std::max(B, 1))) : nvb), B);
     for (int pass = dry ? 0 : 1; pass < 2; ++pass) {
 #define SFM_NMS_STREAM(S, T)                                                                                 \
   if (SHr == S && NTr == T)                                                                                  \
@@ -421,17 +429,18 @@ static void launch_tile(const float* R, const MedianState* state, uint64_t* cand
 }
 
 void launch_nms(const float* R, const MedianState* state, uint64_t* cand,
-                unsigned long long* cand_count, int B, int H, int W, int ksize, int mode, hipStream_t st) {
+                unsigned long long* cand_count, int B, int H, int W, int ksize, int mode, hipStream_t st,
+                int force_tile) {
   const int kh = ksize / 2;
   const int tiles_x = (W + kNT_W - 1) / kNT_W;
   const int tiles_y = (H + kNT_H - 1) / kNT_H;
   const int ntiles = tiles_x * tiles_y;
   switch (kh) {
-    case 0: launch_tile<0>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st); break;
-    case 1: launch_tile<1>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st); break;
-    case 2: launch_tile<2>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st); break;
-    case 3: launch_tile<3>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st); break;
-    case 4: launch_tile<4>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st); break;
+    case 0: launch_tile<0>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st, force_tile); break;
+    case 1: launch_tile<1>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st, force_tile); break;
+    case 2: launch_tile<2>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st, force_tile); break;
+    case 3: launch_tile<3>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st, force_tile); break;
+    case 4: launch_tile<4>(R, state, cand, cand_count, B, H, W, tiles_x, mode, st, force_tile); break;
     default: {
       dim3 grid(std::min(ntiles, kNmsBlocksPerPlane), B);
       hipLaunchKernelGGL(k_nms_generic<SFM_NMS_MAX_HALF>, grid, dim3(256), 0, st, R, state, cand, cand_count, H, W,
