@@ -153,7 +153,9 @@ void launch_ingest_rgb(const uint8_t* rgb, uint8_t* tmp, float* gray, const int3
                        int B, int H, int W, int H2, int W2, hipStream_t st);
 // levels l+1..l+3 of exact 2x steps in one pass; false (nothing launched) when the sizes or
 // alignments do not allow it
-bool launch_down2x3(const float* src, int sh, int sw, float* d1, float* d2, float* d3, int B, hipStream_t st);
+// z0 / z1 (optional, 16-B aligned, multiples of 16 B): buffers the launch zeroes on the side
+bool launch_down2x3(const float* src, int sh, int sw, float* d1, float* d2, float* d3, int B, hipStream_t st,
+                    void* z0 = nullptr, size_t z0_bytes = 0, void* z1 = nullptr, size_t z1_bytes = 0);
 void launch_resize(const float* src, int sh, int sw, float* dst, int dh, int dw, int B,
                    hipStream_t st);
 

@@ -6,6 +6,8 @@
 //   * exact 2x in both axes -> OpenCV's INTER_AREA-fast switch: ((a00+a01)+(a10+a11))*0.25
 //   * otherwise half-pixel bilinear with OpenCV's coefficient rule.
 // Planes of all B images of one level are contiguous: [B][h][w] float32.
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace sfm {
@@ -70,7 +72,15 @@ SFM_DEV float down2_px(float a00, float a01, float a10, float a11) {
 
 __global__ void __launch_bounds__(256) k_down2x3(const float* __restrict__ src, int sh, int sw,
                                                  float* __restrict__ d1, float* __restrict__ d2,
-                                                 float* __restrict__ d3, int B) {
+                                                 float* __restrict__ d3, int B, uint4* __restrict__ z0,
+                                                 int64_t n0, uint4* __restrict__ z1, int64_t n1) {
+  // side job: zero the extraction's histograms and counters (z0 / z1, 16-B units), so the
+  // step needs no separate fill launches ahead of Harris
+  {
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = i0; i < n0; i += gs) z0[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int64_t i = i0; i < n1; i += gs) z1[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
   const int bw = sw >> 3, bh = sh >> 3;
   const int w1 = sw >> 1, w2 = sw >> 2, w3 = sw >> 3;
   const int h1 = sh >> 1, h2 = sh >> 2, h3 = sh >> 3;
@@ -112,12 +122,16 @@ __global__ void __launch_bounds__(256) k_down2x3(const float* __restrict__ src, 
   }
 }
 
-bool launch_down2x3(const float* src, int sh, int sw, float* d1, float* d2, float* d3, int B, hipStream_t st) {
+bool launch_down2x3(const float* src, int sh, int sw, float* d1, float* d2, float* d3, int B, hipStream_t st,
+                    void* z0, size_t z0_bytes, void* z1, size_t z1_bytes) {
   const bool ok = sh % 8 == 0 && sw % 8 == 0 && sh >= 8 && sw >= 8 && ((uintptr_t)src & 15) == 0 &&
-                  ((uintptr_t)d1 & 15) == 0 && ((uintptr_t)d2 & 7) == 0;
+                  ((uintptr_t)d1 & 15) == 0 && ((uintptr_t)d2 & 7) == 0 && ((uintptr_t)z0 & 15) == 0 &&
+                  ((uintptr_t)z1 & 15) == 0 && z0_bytes % 16 == 0 && z1_bytes % 16 == 0;
   if (!ok) return false;
   const int64_t n = (int64_t)B * (sh / 8) * (sw / 8);
-  hipLaunchKernelGGL(k_down2x3, dim3(grid_for(n, 1)), dim3(256), 0, st, src, sh, sw, d1, d2, d3, B);
+  const int64_t n0 = z0 ? (int64_t)(z0_bytes / 16) : 0, n1 = z1 ? (int64_t)(z1_bytes / 16) : 0;
+  hipLaunchKernelGGL(k_down2x3, dim3(grid_for(std::max(n, std::max(n0, n1)), 1)), dim3(256), 0, st, src, sh, sw,
+                     d1, d2, d3, B, static_cast<uint4*>(z0), n0, static_cast<uint4*>(z1), n1);
   return true;
 }
 

@@ -241,6 +241,13 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   // pyramid
   std::vector<const float*> lvl(L);
   lvl[0] = imgs;
+  // the first three-level pyramid pass also zeroes the histograms and append counters
+  const size_t hist_bytes = (size_t)L * B * kMedBins1 * 4, count_bytes = (size_t)4 * L * B * 8 * kCounterStride;
+  static const bool fill_launches = [] {  // SFMFEAT_FILL_LAUNCHES=1: separate fills (A/B)
+    const char* e = getenv("SFMFEAT_FILL_LAUNCHES");
+    return e && atoi(e) != 0;
+  }();
+  bool zeroed = fill_launches;
   {
     StageScope sc(c, SFM_PROF_PYRAMID, st);
     int64_t off = 0;
@@ -255,7 +262,9 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
       const bool x2 = l + 2 < L && lv[l].h * 2 == s.h && lv[l].w * 2 == s.w && lv[l + 1].h * 4 == s.h &&
                       lv[l + 1].w * 4 == s.w && lv[l + 2].h * 8 == s.h && lv[l + 2].w * 8 == s.w;
       if (x2 && launch_down2x3(lvl[l - 1], s.h, s.w, const_cast<float*>(lvl[l]), const_cast<float*>(lvl[l + 1]),
-                               const_cast<float*>(lvl[l + 2]), B, st)) {
+                               const_cast<float*>(lvl[l + 2]), B, st, zeroed ? nullptr : c->d_hist.p, hist_bytes,
+                               zeroed ? nullptr : c->d_counts.p, count_bytes)) {
+        zeroed = true;
         l += 3;
         continue;
       }
@@ -263,8 +272,10 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
       ++l;
     }
   }
-  HIPCHK(c, hipMemsetAsync(c->d_hist.p, 0, (size_t)L * B * kMedBins1 * 4, st));
-  HIPCHK(c, hipMemsetAsync(c->d_counts.p, 0, (size_t)4 * L * B * 8 * kCounterStride, st));
+  if (!zeroed || fill_launches) {
+    HIPCHK(c, hipMemsetAsync(c->d_hist.p, 0, hist_bytes, st));
+    HIPCHK(c, hipMemsetAsync(c->d_counts.p, 0, count_bytes, st));
+  }
   unsigned long long* medcnt = as<unsigned long long>(c->d_counts);
   unsigned long long* candcnt = medcnt + (size_t)L * B * kCounterStride;    // certified NMS
   unsigned long long* candcnt2 = candcnt + (size_t)L * B * kCounterStride;  // fallback NMS
