@@ -224,6 +224,15 @@ int32_t sfm_match_pairs_dev(sfm_ctx* ctx, const float* desc, const int32_t* coun
  *    calls on this ctx (same table, descriptors unchanged since) — sfm_match_pairs_dev
  *    without its prep of every slot.
  * Results are identical to sfm_match_pairs_dev.  Same pairs / outputs / status rules.
+ * A prepped call whose table (desc, count, nimg, cap) is not the one last prepped on this
+ * ctx returns SFM_ESTATE.  That every slot the device-resident pairs touch was prepped,
+ * and that its descriptors did not change since, is the caller's (unchecked) contract.
+ *
+ * Matcher workspace (both calls): operands 520 B per slot (x capP = cap rounded up to
+ * 128) for the table, plus per pair cap x 532 B (row results, overflow list and 128
+ * admitted-target words per query row).  The per-pair part is bounded: a call with more
+ * pairs than fit the budget (default 2 GiB, env SFMFEAT_MATCH_BUDGET_MB read at context
+ * creation) runs as consecutive sub-launches over the same buffers.
  */
 int32_t sfm_match_prep_dev(sfm_ctx* ctx, const float* desc, const int32_t* count, int32_t nimg,
                            int64_t cap, int32_t slot_lo, int32_t slot_n, void* stream);

@@ -66,9 +66,16 @@ struct sfm_ctx {
   DevBuf i_colmap, i_sets;          // row path (k_rows_h): column map + tap sets
   int i_nsets = 0;
   bool i_rows = false;
+  // the table the matcher operands were last prepped for (sfm_match_prep_dev): a prepped
+  // match call on any other table is SFM_ESTATE
+  const float* prep_desc = nullptr;
+  const int32_t* prep_count = nullptr;
+  int prep_nimg = -1;
+  int64_t prep_cap = -1;
   bool match_direct = false;  // SFMFEAT_MATCH_DIRECT=1: all-pairs exact VALU kernel (A/B checks)
   bool exact_select = false;
-  bool serial = false;        // SFMFEAT_SERIAL=1: no aux-stream overlap (diagnostic timings)  // SFMFEAT_SELECT=exact: every plane takes the exact-median path
+  bool serial = false;        // SFMFEAT_SERIAL=1: no aux-stream overlap (diagnostic timings)
+  size_t match_budget = (size_t)2048 << 20;  // SFMFEAT_MATCH_BUDGET_MB: matcher per-pair workspace bound
   int last_B = 0;             // planes per level of the last extraction
   // stage profiling (sfm_profile_*): HIP events bracketing each stage's launches
   bool prof = false;
@@ -411,6 +418,10 @@ int match_prep_range(sfm_ctx* c, const float* desc, const int32_t* count, int ni
   if (lo < 0 || n < 0 || lo + n > nimg) return set_err(c, SFM_EINVAL, "prep slot range outside the table");
   int rc;
   const float* d0 = desc + (int64_t)lo * cap * 128;
+  c->prep_desc = desc;
+  c->prep_count = count;
+  c->prep_nimg = nimg;
+  c->prep_cap = cap;
   if (c->match_direct) {
     const int64_t capP = (cap + 63) / 64 * 64;
     if ((rc = ensure(c, c->m_descT, (size_t)nimg * 128 * capP * 4))) return rc;
@@ -444,39 +455,51 @@ int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, in
   int rc;
   if (prep) {
     if ((rc = match_prep_range(c, desc, count, nimg, cap, 0, nimg, st))) return rc;
-  } else {  // operands from earlier sfm_match_prep_dev calls: the buffers must cover the table
-    const int64_t capP = c->match_direct ? (cap + 63) / 64 * 64 : (cap + 127) / 128 * 128;
-    const size_t need = c->match_direct ? (size_t)nimg * 128 * capP * 4 : (size_t)nimg * capP * 128 * 2;
-    if ((c->match_direct ? c->m_descT.bytes : c->m_hi.bytes) < need)
-      return set_err(c, SFM_ESTATE, "sfm_match_pairs_prepped_dev before sfm_match_prep_dev for this table");
+  } else {  // operands from earlier sfm_match_prep_dev calls on this same table
+    // (which slots the device-resident pairs touch, and whether their descriptors changed
+    // since, cannot be checked without a host sync: that part is the caller's contract)
+    if (c->prep_desc != desc || c->prep_count != count || c->prep_nimg != nimg || c->prep_cap != cap)
+      return set_err(c, SFM_ESTATE, "sfm_match_pairs_prepped_dev: this table was not the last one prepped "
+                                    "(sfm_match_prep_dev) on this context");
   }
-  if ((rc = ensure(c, c->m_rows, (size_t)P * cap * sizeof(RowBest)))) return rc;
-  if ((rc = ensure(c, c->m_ovf, (size_t)P * cap * sizeof(int2)))) return rc;
+  // Per-pair workspace (row results, overflow list and, for the MFMA sweep, kMatchCandCap
+  // admitted targets per query row: 512 B per row) is bounded: large P runs as consecutive
+  // sub-launches over a fixed budget (SFMFEAT_MATCH_BUDGET_MB, default 2048) instead of one
+  // allocation that grows with P * cap.
+  const size_t budget = c->match_budget;
+  const size_t per_pair = (size_t)cap * (sizeof(RowBest) + sizeof(int2) + (c->match_direct ? 0 : kMatchCandCap * 4 + 8));
+  const int Pmax = (int)std::max<size_t>(1, std::min<size_t>((size_t)P, budget / per_pair));
+  if ((rc = ensure(c, c->m_rows, (size_t)Pmax * cap * sizeof(RowBest)))) return rc;
+  if ((rc = ensure(c, c->m_ovf, (size_t)Pmax * cap * sizeof(int2)))) return rc;
   if (c->m_ovfc.bytes == 0) {  // the overflow counter starts at zero; k_match_compact re-zeroes it
     if ((rc = ensure(c, c->m_ovfc, 16))) return rc;
     HIPCHK(c, hipMemsetAsync(c->m_ovfc.p, 0, 16, st));
   }
   if (!c->match_direct) {  // admitted-target lists of the MFMA sweep (kMatchCandCap per row)
-    if ((rc = ensure(c, c->m_cand, (size_t)P * cap * kMatchCandCap * 4))) return rc;
-    if ((rc = ensure(c, c->m_candn, (size_t)P * cap * 4))) return rc;
-    if ((rc = ensure(c, c->m_candt, (size_t)P * cap * 4))) return rc;
+    if ((rc = ensure(c, c->m_cand, (size_t)Pmax * cap * kMatchCandCap * 4))) return rc;
+    if ((rc = ensure(c, c->m_candn, (size_t)Pmax * cap * 4))) return rc;
+    if ((rc = ensure(c, c->m_candt, (size_t)Pmax * cap * 4))) return rc;
   }
-  if (c->match_direct) {
-    const int64_t capP = (cap + 63) / 64 * 64;
-    StageScope sc(c, SFM_PROF_MATCH, st);
-    launch_match_rows(as<float>(c->m_descT), count, capP, pairs, P, ratio, as<RowBest>(c->m_rows), (int)cap, st);
-  } else {
-    const int64_t capP = (cap + 127) / 128 * 128;
-    StageScope sc(c, SFM_PROF_MATCH, st);
-    launch_match_mfma(desc, count, cap, capP, as<_Float16>(c->m_hi), as<_Float16>(c->m_lo), as<float>(c->m_norm2),
-                      as<float>(c->m_rnorm), as<unsigned int>(c->m_imgmax), pairs, P, ratio, as<RowBest>(c->m_rows),
-                      (int)cap, as<uint32_t>(c->m_cand), as<int32_t>(c->m_candn), as<float>(c->m_candt), as<int>(c->m_ovfc),
-                      as<int2>(c->m_ovf), st);
-  }
-  {
-    StageScope sc(c, SFM_PROF_MATCH_POST, st);
-    launch_match_compact(as<RowBest>(c->m_rows), count, pairs, P, (int)cap, cap, matches, conf, nmatch,
-                         c->match_direct ? nullptr : as<int>(c->m_ovfc), st);
+  for (int p0 = 0; p0 < P; p0 += Pmax) {
+    const int Pn = std::min(Pmax, P - p0);
+    const int32_t* pr = pairs + 2 * (int64_t)p0;
+    if (c->match_direct) {
+      const int64_t capP = (cap + 63) / 64 * 64;
+      StageScope sc(c, SFM_PROF_MATCH, st);
+      launch_match_rows(as<float>(c->m_descT), count, capP, pr, Pn, ratio, as<RowBest>(c->m_rows), (int)cap, st);
+    } else {
+      const int64_t capP = (cap + 127) / 128 * 128;
+      StageScope sc(c, SFM_PROF_MATCH, st);
+      launch_match_mfma(desc, count, cap, capP, as<_Float16>(c->m_hi), as<_Float16>(c->m_lo), as<float>(c->m_norm2),
+                        as<float>(c->m_rnorm), as<unsigned int>(c->m_imgmax), pr, Pn, ratio, as<RowBest>(c->m_rows),
+                        (int)cap, as<uint32_t>(c->m_cand), as<int32_t>(c->m_candn), as<float>(c->m_candt),
+                        as<int>(c->m_ovfc), as<int2>(c->m_ovf), st);
+    }
+    {
+      StageScope sc(c, SFM_PROF_MATCH_POST, st);
+      launch_match_compact(as<RowBest>(c->m_rows), count, pr, Pn, (int)cap, cap, matches + (int64_t)p0 * cap * 2,
+                           conf + (int64_t)p0 * cap, nmatch + p0, c->match_direct ? nullptr : as<int>(c->m_ovfc), st);
+    }
   }
   HIPCHK(c, hipGetLastError());
   return SFM_OK;
@@ -552,6 +575,8 @@ int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out) {
     c->exact_select = se && strcmp(se, "exact") == 0;
     const char* sr = getenv("SFMFEAT_SERIAL");
     c->serial = sr && sr[0] == '1';
+    const char* mb = getenv("SFMFEAT_MATCH_BUDGET_MB");
+    if (mb && atoi(mb) > 0) c->match_budget = (size_t)atoi(mb) << 20;
   }
   c->cap = (int64_t)c->L * k;
   int gs = p->gaussian_size;

@@ -203,20 +203,254 @@ class GatherPlan:
         return inv
 
 
-def allgather_chunk(dist, table, plan: GatherPlan, c: int, src, async_op: bool = False, group=None):
+def allgather_chunk(dist, table, plan: GatherPlan, c: int, src, async_op: bool = False, group=None,
+                    coalesce: bool = False):
     """All-gather chunk c: every rank's `src` slots [0, bc) (its freshly extracted chunk)
-    land in the chunk's table region, rank-major.  One collective per field (xy, desc,
-    count).  With async_op the work handles are returned; `w.wait()` under a stream
-    makes that stream wait for the collective without blocking the host (RCCL)."""
+    land in the chunk's table region, rank-major.  One all_gather_into_tensor per field
+    (desc, xy, count); with `coalesce` the three are issued as ONE grouped RCCL operation
+    (torch's coalescing manager -> ncclGroupStart/End: one launch, one completion per
+    chunk).  Coalescing is for the nccl backend only: gloo's coalesced all-gather mixes
+    the fields' dtypes.  With async_op the work handles are returned; `w.wait()` under a
+    stream makes that stream wait for the collective without blocking the host (RCCL)."""
     bc = plan.chunk_size(c)
     base = plan.chunk_base(c)
     n = plan.world * bc
+    fields = ((table.desc, src.desc), (table.xy, src.xy), (table.count, src.count))
+    if coalesce:
+        with dist._coalescing_manager(group, async_ops=async_op) as cm:
+            for f_out, f_in in fields:
+                dist.all_gather_into_tensor(f_out[base:base + n], f_in[:bc], group=group)
+        return [cm] if async_op else []
     works = []
-    for f_out, f_in in ((table.xy, src.xy), (table.desc, src.desc), (table.count, src.count)):
+    for f_out, f_in in fields:
         w = dist.all_gather_into_tensor(f_out[base:base + n], f_in[:bc], group=group, async_op=async_op)
         if async_op:
             works.append(w)
     return works
+
+
+def slot_checksums(torch, slots, idx=None):
+    """[n, 3] int64 per-slot checksums (desc bits, xy, count; each a position-weighted sum,
+    so a moved or permuted slot changes it) of slots `idx` (default: all) — exact integer
+    arithmetic on the device, used to verify the exchange bit for bit."""
+    if idx is None:
+        idx = torch.arange(slots.count.shape[0], device=slots.count.device)
+    out = []
+    for a in range(0, idx.shape[0], 64):  # bounded int64 temporaries
+        i = idx[a:a + 64]
+        n = i.shape[0]
+        db = slots.desc[i].reshape(n, -1).view(torch.int32).to(torch.int64)
+        w = torch.arange(1, db.shape[1] + 1, device=db.device, dtype=torch.int64)
+        xb = slots.xy[i].reshape(n, -1).to(torch.int64)
+        wx = torch.arange(1, xb.shape[1] + 1, device=xb.device, dtype=torch.int64)
+        out.append(torch.stack([(db * w).sum(1), (xb * wx).sum(1), slots.count[i].to(torch.int64)], dim=1))
+    if not out:
+        return torch.zeros((0, 3), dtype=torch.int64, device=slots.count.device)
+    return torch.cat(out)
+
+
+class ChunkedGatherJob:
+    """BASELINE configs[3] on one rank (Runner.py:183-191 is the schedule it
+    replaces): this rank's S = n_global / world frames extracted in `plan.chunk`-frame
+    chunks with `inflight` chunks on the GPU at once (one context + stream per lane); each
+    chunk's slot table is all-gathered over RCCL into the chunk-major global table
+    (GatherPlan) as soon as it is extracted, so the gather of chunk c overlaps the
+    extraction of chunk c+1; the pairs that become ready with chunk c get their matcher
+    operands prepped once and are matched on their own stream (`sfm_match_prep_dev` +
+    `sfm_match_pairs_prepped_dev`) while later chunks are still being extracted.
+
+    exchange='halo' replaces the all-gather by the 1-slot point-to-point halo (consecutive
+    pairs need only rank r+1's first frame); world 1 extracts straight into the table.
+
+    `run(frames)` enqueues one whole job on the caller's stream (no host sync, except for
+    'all' pairs, whose deal needs the gathered counts).  Results: `table` (the global
+    slot table), `sched` (per chunk: the table-slot pairs this rank matched) and `outs`
+    (per chunk: matches, conf, nmatch)."""
+
+    def __init__(self, extractor_params: dict | None, ratio: float, plan: GatherPlan, rank: int, H: int, W: int,
+                 dist=None, inflight: int = 2, exchange: str = "allgather", device: int = 0, group=None,
+                 coalesce: bool | None = None):
+        import torch
+        from .pipeline import BatchExtractor, BatchMatcher, SlotTable
+        self.torch, self.plan, self.rank, self.dist, self.group = torch, plan, rank, dist, group
+        world = plan.world
+        if world > 1 and dist is None:
+            raise ValueError("a multi-rank job needs torch.distributed")
+        self.halo = exchange == "halo"
+        if exchange not in ("allgather", "halo"):
+            raise ValueError(f"unknown exchange {exchange!r}")
+        if self.halo and plan.pairs_mode != "consecutive":
+            raise ValueError("the halo exchange serves consecutive pairs only")
+        if coalesce is None:  # one grouped collective per chunk on RCCL
+            coalesce = world > 1 and dist.get_backend(group) == "nccl"
+        self.coalesce = bool(coalesce)
+        dev = torch.device("cuda", device)
+        self.dev = dev
+        Bx, S, C = plan.chunk, plan.S, plan.C
+        self.lanes = []
+        for _ in range(max(1, inflight)):
+            ex = BatchExtractor(extractor_params, device=device)
+            ex.reserve(Bx, H, W)
+            self.lanes.append({"ex": ex, "stream": torch.cuda.Stream(device=dev), "pending": None})
+        cap = self.cap = self.lanes[0]["ex"].cap
+        self.matcher = BatchMatcher(ratio, device=device)  # own context: matches run on their own stream
+        self.mstream = torch.cuda.Stream(device=dev)
+        if self.halo:
+            # local table: slots [0, S) = own frames in order, slot S = rank r+1's first frame
+            self.table = SlotTable(torch, S + 1, cap, dev)
+            lp = local_consecutive_pairs(S, rank, world)
+            ready = np.minimum(lp[:, 1] // Bx, C - 1)  # pair (l, l+1) is ready with l+1's chunk
+            self.sched = [lp[ready == c] for c in range(C)]
+            self.rank_pairs_n = len(lp)
+        else:
+            self.table = SlotTable(torch, plan.n, cap, dev)
+            if plan.pairs_mode == "all":
+                self.sched = None
+                self.rank_pairs_n = None
+            else:
+                rp = plan.rank_pairs(rank)
+                self.sched = plan.schedule(rp)
+                self.rank_pairs_n = len(rp)
+        for ln in self.lanes:
+            ln["slots"] = SlotTable(torch, Bx, cap, dev) if world > 1 and not self.halo else None
+        self.CH = 4096  # 'all': pairs per matcher launch (output buffer reused)
+        if self.sched is not None:
+            self.sched_dev = [torch.from_numpy(np.ascontiguousarray(p, np.int32)).to(dev) for p in self.sched]
+            self.outs = [self._new_out(len(p)) for p in self.sched]
+        else:
+            self.out_all = self._new_out(self.CH)
+        self.all_pairs = plan.global_pairs() if plan.pairs_mode == "all" else None
+        self.pairs_matched = self.rank_pairs_n
+        self.slot_bytes = cap * (128 * 4 + 2 * 4) + 4
+        self.sent_ck = None
+
+    def _new_out(self, P):
+        torch, cap, dev = self.torch, self.cap, self.dev
+        P = max(P, 1)
+        return (torch.zeros((P, cap, 2), dtype=torch.int32, device=dev),
+                torch.zeros((P, cap), dtype=torch.float32, device=dev),
+                torch.zeros((P,), dtype=torch.int32, device=dev))
+
+    def _view(self, tab, lo, n):
+        from .pipeline import SlotTable
+        v = SlotTable.__new__(SlotTable)
+        v.B, v.cap = n, tab.cap
+        v.xy, v.desc, v.count = tab.xy[lo:lo + n], tab.desc[lo:lo + n], tab.count[lo:lo + n]
+        return v
+
+    def gather_chunk(self, c, src):
+        return allgather_chunk(self.dist, self.table, self.plan, c, src, async_op=True, group=self.group,
+                               coalesce=self.coalesce)
+
+    def run(self, frames, exchange: bool = True, record_sent: bool = False):
+        """Enqueue one job over this rank's frames [S, H, W] (u8 or f32, device-resident).
+        exchange=False skips the collectives (timing of the compute alone: the matcher then
+        reads whatever the table holds).  record_sent keeps per-frame checksums of the slots
+        this rank sends (`verify_exchange`)."""
+        torch, plan, dist = self.torch, self.plan, self.dist
+        world, rank, Bx, C = plan.world, self.rank, plan.chunk, plan.C
+        assert frames.shape[0] == plan.S and frames.is_cuda and frames.is_contiguous()
+        cur = torch.cuda.current_stream()
+        if record_sent:
+            self.sent_ck = torch.zeros((plan.n, 3), dtype=torch.int64, device=self.dev)
+        for ln in self.lanes:
+            ln["stream"].wait_stream(cur)
+            ln["pending"] = None
+        self.mstream.wait_stream(cur)
+        for c in range(C):
+            ln = self.lanes[c % len(self.lanes)]
+            bc = plan.chunk_size(c)
+            l0 = c * Bx
+            works = None
+            with torch.cuda.stream(ln["stream"]):
+                if ln["pending"]:  # the lane's slots are free again once their gather is done
+                    for w in ln["pending"]:
+                        w.wait()
+                    ln["pending"] = None
+                if self.halo:
+                    ln["ex"].extract(frames[l0:l0 + bc], out=self._view(self.table, l0, bc))
+                    if c == 0 and world > 1 and exchange:
+                        halo_exchange(dist, self.table, plan.S, rank, world, self.group)
+                elif world == 1:
+                    ln["ex"].extract(frames[l0:l0 + bc], out=self._view(self.table, plan.chunk_base(c), bc))
+                else:
+                    ln["ex"].extract(frames[l0:l0 + bc], out=self._view(ln["slots"], 0, bc))
+                    if record_sent:
+                        g0 = plan.local_frames(rank, c)[0]
+                        self.sent_ck[g0:g0 + bc] = slot_checksums(torch, self._view(ln["slots"], 0, bc))
+                    if exchange:
+                        works = self.gather_chunk(c, ln["slots"])
+                        ln["pending"] = works
+            if self.sched is None:
+                continue
+            with torch.cuda.stream(self.mstream):
+                if works:
+                    for w in works:
+                        w.wait()
+                elif self.halo and c == C - 1:  # the halo slot arrived on chunk 0's lane
+                    for other in self.lanes:
+                        self.mstream.wait_stream(other["stream"])
+                else:
+                    self.mstream.wait_stream(ln["stream"])
+                # this chunk's slots get their matcher operands once; pairs of earlier
+                # chunks' slots reuse theirs
+                if self.halo:
+                    self.matcher.prep(self.table, l0, bc + (1 if c == C - 1 and world > 1 else 0))
+                else:
+                    self.matcher.prep(self.table, plan.chunk_base(c), world * bc)
+                if len(self.sched[c]):
+                    self.matcher.match(self.table, self.sched_dev[c], out=self.outs[c], prepped=True)
+        for ln in self.lanes:
+            cur.wait_stream(ln["stream"])
+            if ln["pending"]:
+                for w in ln["pending"]:
+                    w.wait()
+                ln["pending"] = None
+        cur.wait_stream(self.mstream)
+        if self.sched is None:  # 'all': deal by cost once the counts are gathered (host sync)
+            counts = self.table.count.cpu().numpy()
+            mine = weighted_deal(self.all_pairs, counts[plan.slot_of(np.arange(plan.n))], world)[rank]
+            sp = torch.from_numpy(plan.slot_of(mine).reshape(-1, 2)).to(self.dev)
+            self.matcher.prep(self.table)
+            out = self.out_all
+            for a in range(0, len(sp), self.CH):
+                n = min(self.CH, len(sp) - a)
+                self.matcher.match(self.table, sp[a:a + n], out=(out[0][:n], out[1][:n], out[2][:n]), prepped=True)
+            self.pairs_matched = len(mine)
+            self.last_all_pairs = sp
+
+    def gather_alone(self, reps: int = 3) -> float:
+        """Seconds per job of the chunked all-gather with nothing else on the GPU (host-timed
+        between barriers)."""
+        import time
+        torch, dist = self.torch, self.dist
+        src = self.lanes[0]["slots"]
+        dist.barrier(group=self.group)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            for c in range(self.plan.C):
+                for w in self.gather_chunk(c, src):
+                    w.wait()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
+    def verify_exchange(self) -> int:
+        """After `run(..., record_sent=True)`: the gathered table holds, at slot_of(g), the
+        exact slot (desc, xy, count) the owner of frame g sent — on every rank.  Sums the
+        owners' checksums over ranks (plain all_reduce) and compares them with checksums of
+        the table.  Returns the number of mismatching frames (0 = bit-exact)."""
+        torch, plan = self.torch, self.plan
+        if self.halo or plan.world == 1:
+            return 0
+        sent = self.sent_ck.clone()
+        self.dist.all_reduce(sent, group=self.group)
+        idx = torch.from_numpy(plan.slot_of(np.arange(plan.n)).astype(np.int64)).to(self.dev)
+        got = slot_checksums(torch, self.table, idx)
+        bad = (got != sent).any(1)
+        nbad = bad.sum().to(torch.int64)
+        self.dist.all_reduce(nbad, group=self.group)
+        return int(nbad.item())
 
 
 def _torch():

@@ -37,7 +37,12 @@ def sample_indices(n: int, iters: int, seed: int = 5) -> np.ndarray:
 
 
 def find_inliers(p1, p2, threshold=1.0, max_iterations=1000, device: int = 0):
-    """Drop-in for CameraPose.find_inliers (SFM.py:126-160)."""
+    """Drop-in for CameraPose.find_inliers (SFM.py:126-160).
+
+    Deliberate divergence: the reference also accepts non-integer coordinates; the device
+    path stores points as int32 (what Runner._convert_matches_to_coords, Runner.py:423-434,
+    produces from the int64 keypoints), so non-integer input raises ValueError instead of
+    being silently truncated."""
     p1 = np.asarray(p1)
     p2 = np.asarray(p2)
     if len(p1) < 8:
@@ -54,7 +59,8 @@ def find_inliers(p1, p2, threshold=1.0, max_iterations=1000, device: int = 0):
 
 def find_inliers_batch(pairs, threshold=1.0, max_iterations=1000, device: int = 0):
     """find_inliers over many correspondence sets in one device pass (one launch set for
-    all pairs; sample streams shared by sets of equal size).  pairs: [(p1, p2), ...];
+    all pairs; sample streams shared by sets of equal size).  Integer coordinates only, as
+    `find_inliers` (a documented divergence).  pairs: [(p1, p2), ...];
     returns the per-pair results of find_inliers."""
     import ctypes
 

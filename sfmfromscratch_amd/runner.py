@@ -33,12 +33,27 @@ def load_image_u8(path: str) -> np.ndarray:
     return a
 
 
+def drop_opaque_alpha(a: np.ndarray, what: str = "frame") -> np.ndarray:
+    """[H, W, 3] RGB view of a decoded RGB or RGBA frame.  The reference reads channels
+    0-2 after `_PIL_resize` (Runner.py:478), and PIL resizes RGBA in premultiplied alpha,
+    so only a fully opaque RGBA frame resizes to the same RGB as its RGB channels alone
+    (checked against PIL in tests/test_ingest_cpu.py).  Translucent RGBA is rejected
+    (ValueError): the device ingest has no premultiplied path (a documented divergence)."""
+    if a.ndim != 3 or a.shape[2] not in (3, 4):
+        raise ValueError(f"{what}: the reference's _rgb2gray needs an [H, W, 3] RGB (or RGBA) frame")
+    if a.shape[2] == 4:
+        if not np.all(a[..., 3] == 255):
+            raise ValueError(f"{what}: translucent RGBA frames are not supported (PIL resizes them premultiplied)")
+        a = a[..., :3]
+    return np.ascontiguousarray(a)
+
+
 def ingest_frame(rgb: np.ndarray, scale_factor: float = 0.5, device: int = 0) -> np.ndarray:
     """Runner.py:33-46 for one decoded frame: resize to (int(W*s), int(H*s)) with PIL's
-    BICUBIC filter, then _rgb2gray; float32 [H2, W2].  The reference indexes three
-    channels (:478), so a non-RGB frame fails there too (here: ValueError)."""
-    if rgb.ndim != 3 or rgb.shape[2] != 3:
-        raise ValueError("the reference's _rgb2gray needs an [H, W, 3] RGB frame")
+    BICUBIC filter, then _rgb2gray; float32 [H2, W2].  A 2-D gray frame fails in the
+    reference's _rgb2gray (:478) and here (ValueError); RGBA frames go through
+    `drop_opaque_alpha`."""
+    rgb = drop_opaque_alpha(rgb)
     ctx = context_for(_abi.params_from_dict({}, _abi.SFM_MODE_NAIVE), device)
     return ctx.ingest_rgb(rgb, scale_factor)
 

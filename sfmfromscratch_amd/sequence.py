@@ -31,7 +31,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .runner import convert_matches_to_coords, load_image_u8
+from .runner import convert_matches_to_coords, drop_opaque_alpha, load_image_u8
 
 
 class Matches:
@@ -85,14 +85,14 @@ class FeatureCache:
         loaded = []
         for f in frames:
             if isinstance(f, str):
-                a = load_image_u8(f)
-                # the reference's _rgb2gray indexes three channels (Runner.py:478): a gray
-                # or RGBA file fails there, so it fails here instead of being extracted at
-                # the wrong scale
-                if a.ndim != 3 or a.shape[2] != 3 or a.dtype != np.uint8:
-                    raise ValueError(f"{f}: the reference's _rgb2gray needs an [H, W, 3] RGB frame")
+                # a 2-D gray file fails in the reference's _rgb2gray (Runner.py:478), so it
+                # fails here instead of being extracted at the wrong scale; opaque RGBA
+                # files work there and here
+                a = drop_opaque_alpha(load_image_u8(f), f)
             else:
                 a = np.asarray(f)
+                if a.ndim == 3:
+                    a = drop_opaque_alpha(a)
                 if a.ndim == 2 and a.dtype != np.float32:
                     raise ValueError("gray frames must be float32 [H, W] in [0, 1] (the extractor's input)")
             loaded.append(a)

@@ -292,19 +292,7 @@ def test_pipeline_batches_in_flight_match_serial():
         assert ln is pipe.lanes[i % 2]
         assert torch.equal(s.count, ln["slots"].count)
         for b, n in enumerate(s.count.tolist()):  # rows past the count are stale in a reused lane
-            a_, c_ = s.xy[b, :n].cpu().numpy(), ln["slots"].xy[b, :n].cpu().numpy()
-            bad = np.nonzero((a_ != c_).any(1))[0]
-            if len(bad):
-                img = batches[i][b].cpu().numpy().astype(np.float32) / np.float32(255)
-                R, med, _ = _native.debug_harris(img, _abi.params_from_dict(pp, _abi.SFM_MODE_SCALEROT))
-                Rs = {(int(x), int(y)): hex(int(np.float32(R[y, x]).view(np.uint32)))
-                      for x, y in a_[bad[:4]].tolist() + c_[bad[:4]].tolist()}
-                s2 = ex.extract(batches[i])
-                torch.cuda.synchronize()
-                again = s2.xy[b, :n].cpu().numpy()
-                raise AssertionError((i, b, n, bad[:8].tolist(), a_[bad[:4]].tolist(), c_[bad[:4]].tolist(), Rs,
-                                      "serial again == serial", bool((again == a_).all()),
-                                      "serial again == lane", bool((again == c_).all())))
+            assert torch.equal(s.xy[b, :n], ln["slots"].xy[b, :n])
             assert torch.equal(s.desc[b, :n], ln["slots"].desc[b, :n])
         assert torch.equal(nm, ln["mout"][2])
         for p in range(B - 1):
@@ -417,4 +405,28 @@ def test_prep_ranges_then_prepped_match_equal_full_match():
     torch.cuda.synchronize()
     for a, b in zip(ref, got):
         assert torch.equal(a, b)
+    # a table other than the one last prepped on this context is refused too
+    s2 = ex.extract(torch.from_numpy(synth.make_batch_u8(B, H, W, seed=94)).cuda())
+    with pytest.raises(RuntimeError):
+        m.match(s2, pairs, prepped=True)
+
+
+def test_match_workspace_budget_sub_launches_equal_one_launch(monkeypatch):
+    """A call with more pairs than the per-pair workspace budget runs as consecutive
+    sub-launches (bounded allocation); the results equal one launch's."""
+    torch = pytest.importorskip("torch")
+    from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, all_pairs
+    B, H, W = 6, 270, 480
+    ex = BatchExtractor(dict(P_OCT, num_interest_points=800))
+    s = ex.extract(torch.from_numpy(synth.make_batch_u8(B, H, W, seed=95)).cuda())
+    pairs = torch.from_numpy(all_pairs(B)).cuda()
+    ref = BatchMatcher(0.85).match(s, pairs)
+    monkeypatch.setenv("SFMFEAT_MATCH_BUDGET_MB", "1")  # ~2 pairs per sub-launch at cap 800
+    small = BatchMatcher(0.85)
+    got = small.match(s, pairs)
+    small.prep(s)
+    got2 = small.match(s, pairs, prepped=True)
+    torch.cuda.synchronize()
+    for a, b, c in zip(ref, got, got2):
+        assert torch.equal(a, b) and torch.equal(a, c)
 

@@ -47,3 +47,24 @@ def test_u8_float_roundtrip_is_exact():
     f = u.astype(np.float64).astype(np.float32) / 255
     f *= 255
     assert np.array_equal(np.uint8(f), u)
+
+
+def test_opaque_rgba_drops_alpha_translucent_rejected():
+    """PIL resizes RGBA premultiplied: an opaque RGBA frame resizes to the same RGB as its
+    RGB channels (so runner.drop_opaque_alpha is exact), a translucent one does not and is
+    rejected (ValueError, the documented divergence)."""
+    from PIL import Image
+
+    from sfmfromscratch_amd.runner import drop_opaque_alpha
+    rng = np.random.default_rng(7)
+    a = rng.integers(0, 256, (37, 53, 4), dtype=np.uint8)
+    a[..., 3] = 255
+    via_rgba = np.asarray(Image.fromarray(a).resize((26, 18)))[..., :3]
+    rgb = drop_opaque_alpha(a)
+    assert rgb.shape == (37, 53, 3) and rgb.flags.c_contiguous
+    assert np.array_equal(via_rgba, np.asarray(Image.fromarray(rgb).resize((26, 18))))
+    a[0, 0, 3] = 254
+    with pytest.raises(ValueError):
+        drop_opaque_alpha(a)
+    with pytest.raises(ValueError):
+        drop_opaque_alpha(a[..., 0])
