@@ -699,6 +699,9 @@ def verify_gather_job(args, torch, dist, dev, job, frame_of, world, rank):
         n = int(s.count[0])
         ok = (n == int(job.table.count[t]) and torch.equal(s.xy[0, :n], job.table.xy[t, :n])
               and torch.equal(s.desc[0, :n], job.table.desc[t, :n]))
+        if not ok:
+            log(f"verify: frame {g} (slot {t}): count {n} vs {int(job.table.count[t])}, xy equal "
+                f"{torch.equal(s.xy[0, :n], job.table.xy[t, :n])}, desc equal {torch.equal(s.desc[0, :n], job.table.desc[t, :n])}")
         bad += 0 if ok else 1
     npairs = 0
     if job.sched is not None and not job.halo:
@@ -714,6 +717,9 @@ def verify_gather_job(args, torch, dist, dev, job, frame_of, world, rank):
                 o = job.outs[c]
                 kk = int(nm[0])
                 ok = kk == int(o[2][k]) and torch.equal(mm[0, :kk], o[0][k, :kk]) and torch.equal(mc[0, :kk], o[1][k, :kk])
+                if not ok:
+                    log(f"verify: chunk {c} pair {k} slots ({a}, {b}): nmatch {kk} vs {int(o[2][k])}, matches equal "
+                        f"{torch.equal(mm[0, :kk], o[0][k, :kk])}, conf equal {torch.equal(mc[0, :kk], o[1][k, :kk])}")
                 bad += 0 if ok else 1
                 npairs += 1
     torch.cuda.synchronize()

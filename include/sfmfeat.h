@@ -285,6 +285,10 @@ float sfm_debug_time_harris(int32_t device, int32_t abl, int32_t B, int32_t H, i
  * (image x level) that took the exact-median path, and planes in total.  The default
  * certified select decides the others from the Harris histogram alone. */
 int32_t sfm_debug_select_stats(sfm_ctx* ctx, int32_t* fallback_planes, int32_t* total_planes);
+/* Level l's R maps (what 0) or level images (what 1) of the last extraction -> out [B][h][w]
+ * (device, on `stream`; diagnostics). */
+int32_t sfm_debug_copy_level(sfm_ctx* ctx, int32_t l, int32_t what, float* out, void* stream);
+
 
 #ifdef __cplusplus
 }

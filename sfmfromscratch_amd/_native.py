@@ -66,6 +66,8 @@ SIGNATURES = {
     "sfm_profile_read": (ctypes.c_int32, [_vp, ctypes.POINTER(ctypes.c_double), _i64p, ctypes.c_int32]),
     "sfm_debug_time_harris": (ctypes.c_float, [ctypes.c_int32] * 6),
     "sfm_debug_select_stats": (ctypes.c_int32, [_vp, _i32p, _i32p]),
+
+    "sfm_debug_copy_level": (ctypes.c_int32, [_vp, ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
     "sfm_debug_atan2": (ctypes.c_int32, [ctypes.c_int32, _fp, _fp, _fp, ctypes.c_int64]),
     "sfm_debug_harris": (ctypes.c_int32, [ctypes.c_int32, _fp, ctypes.c_int32, ctypes.c_double, ctypes.c_int32,
                                           _fp, ctypes.c_int32, ctypes.c_int32, _fp, _fp, _i64p]),
@@ -187,6 +189,11 @@ class Context:
         fb, tot = ctypes.c_int32(0), ctypes.c_int32(0)
         check(self.lib.sfm_debug_select_stats(self.handle, ctypes.byref(fb), ctypes.byref(tot)), self.handle)
         return int(fb.value), int(tot.value)
+
+    def copy_level(self, level: int, what: int, out_ptr: int, stream: int):
+        """Level `level`'s R maps (what 0) / images (what 1) of the last extraction -> out."""
+        check(self.lib.sfm_debug_copy_level(self.handle, int(level), int(what), ctypes.c_void_p(out_ptr),
+                                            ctypes.c_void_p(stream)), self.handle)
 
     # -------- host-pointer API (drop-in path) --------
     def extract(self, img: np.ndarray):

@@ -27,8 +27,9 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kQW = 32;                // query rows per wave
-constexpr int kWaves = 4;              // waves per workgroup
-constexpr int kQB = kQW * kWaves;      // 128 query rows per workgroup
+constexpr int kWaves = 8;              // waves per workgroup (two per SIMD: one workgroup per CU)
+constexpr int kQB = kQW * kWaves;      // 256 query rows per workgroup
+constexpr int kNT = 64 * kWaves;       // threads per workgroup
 constexpr int kRowH = 128 + 8;         // padded fp16 row in LDS (272 B): conflict-free b128 reads
 constexpr int kCandCap = kMatchCandCap;  // admitted targets per query row (global list)
 constexpr int kHalfCap = kCandCap / 2;   // each half-wave's share of a row's list
@@ -153,6 +154,14 @@ SFM_DEV void top2_merge(float& b1, int& j1, float& b2, float ob1, int oj1, float
 
 constexpr int kTT2 = 64;               // targets per LDS stage (two 32-target MFMA sub-tiles)
 constexpr int kStageHalves = kTT2 * kRowH;  // f16 elements per array per stage
+// LDS of one sweep workgroup: two stage buffers (hi, lo) + target norms (three stages) + the
+// per-wave d~ staging of the appends.  Over 160 KB - sizeof(k_harris's LDS) on purpose: a sweep
+// workgroup then never shares a CU with a Harris workgroup of a concurrent extraction (two
+// streams).  On gfx950 that pairing corrupted ~0.3 % of k_harris's v_pk_fma_f32 results
+// (tools/check_c4b.py; the inputs verified unchanged inside the kernel), so the exclusion is by
+// construction, and one 512-thread workgroup per CU keeps two waves per SIMD.
+constexpr size_t kSweepLds = 2 * 2 * kStageHalves * 2 + 3 * kTT2 * 4 + kWaves * 64 * 16 * 4;
+static_assert(kSweepLds > 160 * 1024 - 71720, "a sweep workgroup must not fit beside a k_harris workgroup");
 
 // One workgroup = 4 waves x 32 query rows; ONE sweep over the target table of the pair in
 // 64-row LDS stages (the next stage's hi/lo rows are loaded into registers while the
@@ -174,14 +183,16 @@ constexpr int kStageHalves = kTT2 * kRowH;  // f16 elements per array per stage
 // ABL (timing builds only; results are wrong unless 0): 9 = no epilogue, 10 = no MFMAs,
 // 11 = no stage loads (every stage reuses stage 0's LDS rows), 12 = no list appends
 template <int ABL>
-__global__ void __launch_bounds__(256, 2) k_match_mfma(
+__global__ void __launch_bounds__(kNT, 1) k_match_mfma(
     const int32_t* __restrict__ count, int64_t capP, const _Float16* __restrict__ hi,
     const _Float16* __restrict__ lo, const float* __restrict__ norm2, const float* __restrict__ rnorm,
     const unsigned int* __restrict__ imgmax, const int32_t* __restrict__ pairs, int P, int max_rows,
     uint32_t* __restrict__ cand, int32_t* __restrict__ cand_n, float* __restrict__ cand_thr,
     int* __restrict__ ovf_count, int2* __restrict__ ovf_list) {
-  __shared__ __attribute__((aligned(16))) _Float16 sT[2][kStageHalves];
-  __shared__ __attribute__((aligned(16))) float sN[2][kTT2];  // target norms, by stage parity
+  // stage buffers: stage st in sT[st & 1] (hi, lo); its target norms in sN[st % 3] (the carried
+  // sub-tile's epilogue reads stage st - 1's norms while stage st + 1's are being stored)
+  __shared__ __attribute__((aligned(16))) _Float16 sT[2][2][kStageHalves];
+  __shared__ __attribute__((aligned(16))) float sN[3][kTT2];
   __shared__ __attribute__((aligned(16))) float sD[kWaves][64][16];  // a sub-tile's d~ per lane
 
   // XCD-aware mapping (workgroups b and b + 8 share an XCD and its L2): group g = b % 8
@@ -222,32 +233,32 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
   const int nst = (n2 + kTT2 - 1) / kTT2;
   const int64_t to = (int64_t)i2 * capP * 128;
   // stage loader: 64 rows x (hi, lo) x 256 B = 32 KB, each array one contiguous 16 KB run;
-  // pass q reads 4 KB of it with consecutive 16-B pieces per lane (one 1 KB run per wave
-  // instruction): thread t -> row 16 q + t / 16, halves 8 (t % 16)
+  // pass q reads 8 KB of it with consecutive 16-B pieces per lane (one 1 KB run per wave
+  // instruction): thread t -> row 32 q + t / 16, halves 8 (t % 16)
   const int lr = tid >> 4, lc = (tid & 15) * 8;
-  h8 g[8];
+  h8 g[4];
   auto load_stage = [&](int st) {
     if (ABL == 11 && st > 0) return;
     const int64_t gofs = to + (int64_t)(st * kTT2) * 128 + tid * 8;  // rows < capP: in bounds
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      g[q] = *reinterpret_cast<const h8*>(hi + gofs + 2048 * q);
-      g[4 + q] = *reinterpret_cast<const h8*>(lo + gofs + 2048 * q);
+    for (int q = 0; q < 2; ++q) {
+      g[q] = *reinterpret_cast<const h8*>(hi + gofs + 4096 * q);
+      g[2 + q] = *reinterpret_cast<const h8*>(lo + gofs + 4096 * q);
     }
   };
-  auto store_stage = [&](bool first) {
+  auto store_stage = [&](int buf, bool first) {
     if (ABL == 11 && !first) return;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      *reinterpret_cast<h8*>(&sT[0][(16 * q + lr) * kRowH + lc]) = g[q];
-      *reinterpret_cast<h8*>(&sT[1][(16 * q + lr) * kRowH + lc]) = g[4 + q];
+    for (int q = 0; q < 2; ++q) {
+      *reinterpret_cast<h8*>(&sT[buf][0][(32 * q + lr) * kRowH + lc]) = g[q];
+      *reinterpret_cast<h8*>(&sT[buf][1][(32 * q + lr) * kRowH + lc]) = g[2 + q];
     }
   };
-  // 32 targets x 32 queries of sub-tile `sub` of the staged rows: hi.hi into ahh, hi.lo +
-  // lo.hi into ax (one accumulation chain each)
-  auto mfma_sub = [&](int sub, f32x16& ahh, f32x16& ax) {
-    const _Float16* tH = &sT[0][0];
-    const _Float16* tL = &sT[1][0];
+  // 32 targets x 32 queries of sub-tile `sub` of the stage in buffer `buf`: hi.hi into ahh,
+  // hi.lo + lo.hi into ax (one accumulation chain each)
+  auto mfma_sub = [&](int buf, int sub, f32x16& ahh, f32x16& ax) {
+    const _Float16* tH = &sT[buf][0][0];
+    const _Float16* tL = &sT[buf][1][0];
     const int trow = (32 * sub + (lane & 31)) * kRowH;
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
@@ -342,26 +353,30 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
 
   load_stage(0);
   const float nrm_t0 = (tid < kTT2) ? norm2[(int64_t)i2 * capP + tid] : 0.0f;
-  store_stage(true);
+  store_stage(0, true);
   if (tid < kTT2) {
     sN[0][tid] = nrm_t0;
-    sN[1][tid] = INFINITY;  // "stage -1": the carried sub-tile's first epilogue is a no-op
+    sN[2][tid] = INFINITY;  // "stage -1": the carried sub-tile's first epilogue is a no-op
   }
   f32x16 ph_hh = {}, ph_x = {};  // carried sub-tile 1 of the previous stage
+  int n3 = 0;                    // st % 3
   for (int st = 0; st < nst; ++st) {
-    __syncthreads();  // stage st visible
+    // stage st (buffer st & 1) is visible, and every wave is done with stage st - 1's rows,
+    // so its buffer takes stage st + 1 below: one barrier per stage
+    __syncthreads();
     // next stage's rows (the last stage re-reads itself: branch-free loop body, so the
     // MFMAs and the epilogue share one scheduling region)
     const int sn = min(st + 1, nst - 1);
     load_stage(sn);
     const float nrm_next = norm2[(int64_t)i2 * capP + sn * kTT2 + (tid & (kTT2 - 1))];
-    const int par = st & 1;
+    const int buf = st & 1;
+    const int np3 = n3 == 0 ? 2 : n3 - 1, nn3 = n3 == 2 ? 0 : n3 + 1;
     {
       float nb[16], d[16];
       uint32_t mm = 0;
       f32x16 h0 = {}, x0 = {};
-      load_nb(par ^ 1, 1, nb);
-      mfma_sub(0, h0, x0);
+      load_nb(np3, 1, nb);
+      mfma_sub(buf, 0, h0, x0);
       epi(ph_hh, ph_x, nb, d, mm);
       interleave();
       pin(b1, b2, mm);
@@ -373,8 +388,8 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
       float nb[16], d[16];
       uint32_t mm = 0;
       f32x16 h1 = {}, x1 = {};
-      load_nb(par, 0, nb);
-      mfma_sub(1, h1, x1);
+      load_nb(n3, 0, nb);
+      mfma_sub(buf, 1, h1, x1);
       epi(ph_hh, ph_x, nb, d, mm);
       interleave();
       pin(b1, b2, mm);
@@ -386,14 +401,14 @@ __global__ void __launch_bounds__(256, 2) k_match_mfma(
       const float ob1 = other_half(b1), ob2 = other_half(b2);
       thr_w = fminf(fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + E2, thr_w);
     }
-    __syncthreads();  // every wave is done with this stage's LDS rows and norms
-    store_stage(false);
-    if (tid < kTT2) sN[par ^ 1][tid] = nrm_next;
+    store_stage(buf ^ 1, false);
+    if (tid < kTT2) sN[nn3][tid] = nrm_next;
+    n3 = nn3;
   }
   {
-    uint32_t mm = 0;  // the last stage's sub-tile 1
+    uint32_t mm = 0;  // the last stage's sub-tile 1 (its norms: stage nst - 1)
     float nb[16], d[16];
-    load_nb((nst - 1) & 1, 1, nb);
+    load_nb(n3 == 0 ? 2 : n3 - 1, 1, nb);
     epi(ph_hh, ph_x, nb, d, mm);
     append(mm, d, (nst - 1) * kTT2 + 32);
   }
@@ -711,7 +726,7 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
   const dim3 grid((unsigned)(8 * ((P + 7) / 8) * qb));
   // ovf_count is zero here: set once at allocation, re-zeroed by k_match_compact
 #define SFM_SWEEP(A)                                                                                           \
-  hipLaunchKernelGGL(k_match_mfma<A>, grid, dim3(256), 0, st, count, capP, hi, lo, norm2, rnorm, imgmax, pairs, P, \
+  hipLaunchKernelGGL(k_match_mfma<A>, grid, dim3(kNT), 0, st, count, capP, hi, lo, norm2, rnorm, imgmax, pairs, P, \
                      max_rows, cand, cand_n, cand_thr, ovf_count, ovf_list)
   if (abl == 9)
     SFM_SWEEP(9);

@@ -77,6 +77,7 @@ struct sfm_ctx {
   bool serial = false;        // SFMFEAT_SERIAL=1: no aux-stream overlap (diagnostic timings)
   size_t match_budget = (size_t)2048 << 20;  // SFMFEAT_MATCH_BUDGET_MB: matcher per-pair workspace bound
   int last_B = 0;             // planes per level of the last extraction
+  int last_H = 0, last_W = 0;
   // stage profiling (sfm_profile_*): HIP events bracketing each stage's launches
   bool prof = false;
   uint32_t prof_mask = ~0u;  // stages bracketed while profiling (sfm_profile_stages)
@@ -245,6 +246,8 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   if (rc) return rc;
   const int L = c->L;
   c->last_B = B;
+  c->last_H = H;
+  c->last_W = W;
   // pyramid
   std::vector<const float*> lvl(L);
   lvl[0] = imgs;
@@ -984,6 +987,22 @@ int32_t sfm_profile_stages(sfm_ctx* c, int32_t mask) {
   if (!c) return SFM_EINVAL;
   c->prof = mask != 0;
   c->prof_mask = (uint32_t)mask;
+  return SFM_OK;
+}
+
+// diagnostics: copy level `l`'s R maps (what = 0) or level images (what = 1) of the last
+// extraction, all planes [B][h][w], to the device buffer `out` on `stream`
+int32_t sfm_debug_copy_level(sfm_ctx* c, int32_t l, int32_t what, float* out, void* stream) {
+  if (!c || !out || l < 0 || l >= c->L || !c->last_B) return SFM_EINVAL;
+  std::vector<Level> lv;
+  if (geometry(&c->p, c->last_H, c->last_W, lv) != SFM_OK) return SFM_EINVAL;
+  const int B = c->last_B;
+  int64_t off = 0, offl = 0;
+  for (int k = 0; k < l; ++k) off += (int64_t)B * lv[k].h * lv[k].w;
+  for (int k = 1; k < l; ++k) offl += (int64_t)B * lv[k].h * lv[k].w;
+  const size_t bytes = (size_t)B * lv[l].h * lv[l].w * 4;
+  const float* src = what == 0 ? as<float>(c->d_R) + off : (l == 0 ? as<float>(c->d_img0) : as<float>(c->d_lvl) + offl);
+  HIPCHK(c, hipMemcpyAsync(out, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return SFM_OK;
 }
 

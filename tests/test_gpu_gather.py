@@ -136,3 +136,60 @@ def test_chunked_gather_job_two_ranks_gloo_vs_oracle(pairs):
         errs.append(errq.get())
     assert not alive, "a rank hung"
     assert not errs and all(p.exitcode == 0 for p in procs), errs
+
+
+P_1080 = dict(P_OCT)  # BASELINE configs[1] parameters, k = 2500
+
+
+def _clean_checksums(torch, frames_u8):
+    """Per-frame slot checksums of a B = 1 extraction of each frame (nothing else on the GPU)."""
+    from sfmfromscratch_amd import distributed as D
+    from sfmfromscratch_amd.pipeline import BatchExtractor
+    ex = BatchExtractor(P_1080)
+    return torch.cat([D.slot_checksums(torch, ex.extract(frames_u8[i:i + 1])) for i in range(frames_u8.shape[0])])
+
+
+def test_chunked_job_1080p_concurrent_matching_equals_clean_extraction():
+    """configs[3]'s job at full size: 1080p chunks extracted on two lanes while the ready pairs
+    are matched on a third stream.  Every gathered slot must equal a clean single-frame
+    extraction of its frame bit for bit (this is the check that caught k_match_mfma and
+    k_harris sharing CUs)."""
+    torch = pytest.importorskip("torch")
+    from sfmfromscratch_amd import distributed as D
+    U, n = 32, 128
+    uq = torch.from_numpy(np.stack([synth.make_frame_u8(1080, 1920, 77, i) for i in range(U)])).cuda()
+    ref = _clean_checksums(torch, uq)
+    frames = uq[torch.arange(n, device="cuda") % U].contiguous()
+    plan = D.GatherPlan(n, 1, 32, "consecutive")
+    job = D.ChunkedGatherJob(P_1080, RATIO, plan, 0, 1080, 1920, inflight=2)
+    for _ in range(2):
+        job.run(frames)
+        torch.cuda.synchronize()
+        got = D.slot_checksums(torch, job.table)
+        bad = (got != ref[torch.arange(n, device="cuda") % U]).any(1).nonzero().flatten().tolist()
+        assert not bad, f"{len(bad)} gathered slots differ from a clean extraction: {bad[:10]}"
+
+
+def test_pipeline_1080p_lanes_equal_clean_extraction():
+    """The headline pipeline (two 32 x 1080p batches in flight, each lane's matcher overlapping
+    the other lane's extraction): every lane's slots after every batch equal a clean
+    single-frame extraction."""
+    torch = pytest.importorskip("torch")
+    from sfmfromscratch_amd import distributed as D
+    from sfmfromscratch_amd.pipeline import BatchPipeline, consecutive_pairs
+    B = 32
+    u8 = torch.from_numpy(np.stack([synth.make_frame_u8(1080, 1920, 78, i) for i in range(B)])).cuda()
+    ref = _clean_checksums(torch, u8)
+    frames = torch.from_numpy(synth.u8_to_gray(u8.cpu().numpy())).cuda()
+    pairs = torch.from_numpy(consecutive_pairs(B)).cuda()
+    pipe = BatchPipeline(P_1080, RATIO, B, 1080, 1920, pairs, inflight=2, extra_slots=1)
+    cks = []
+    for _ in range(6):
+        ln = pipe.submit(frames)
+        with torch.cuda.stream(ln["stream"]):
+            cks.append(D.slot_checksums(torch, ln["view"]))
+    pipe.join()
+    torch.cuda.synchronize()
+    for s, ck in enumerate(cks):
+        bad = (ck != ref).any(1).nonzero().flatten().tolist()
+        assert not bad, f"batch {s}: {len(bad)} frames differ from a clean extraction: {bad[:10]}"
