@@ -209,11 +209,18 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
                                                    int kcap, const int32_t* __restrict__ lc_all, int level,
                                                    int B, double scale, int32_t* __restrict__ out_xy,
                                                    float* __restrict__ out_desc, float* __restrict__ out_conf,
-                                                   int64_t out_cap) {
+                                                   int64_t out_cap, int32_t* __restrict__ out_count, int L) {
   using C = Geo<WS, ROT>;
   constexpr int N = C::N, PW = C::PW, NP = C::NP, E = C::E, RN = C::RN, h = WS / 2;
   __shared__ __attribute__((aligned(16))) float s_all[4 * C::G];
   const int b = blockIdx.y;
+  // the last level's launch also writes the slot's keypoint count (sum over the levels), so
+  // no separate one-workgroup finalize launch trails the extraction
+  if (out_count != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+    int32_t s = 0;
+    for (int l = 0; l < L; ++l) s += lc_all[(int64_t)l * B + b];
+    out_count[b] = s;
+  }
   const int count = kp.count[b];
   const int kbase = blockIdx.x * 4;
   if (kbase >= count) return;
@@ -534,10 +541,10 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
 #define SFM_DQ_BODY(WS)                                                                              \
     if (rotate)                                                                                      \
       hipLaunchKernelGGL((dq::k_describe_q<WS, 1>), grid, dim3(64), 0, st, lvl, H, W, kp, kcap, lc,  \
-                         level, B, scale, out_xy, out_desc, out_conf, out_cap);                      \
+                         level, B, scale, out_xy, out_desc, out_conf, out_cap, out_count, L);        \
     else                                                                                             \
       hipLaunchKernelGGL((dq::k_describe_q<WS, 0>), grid, dim3(64), 0, st, lvl, H, W, kp, kcap, lc,  \
-                         level, B, scale, out_xy, out_desc, out_conf, out_cap);                      \
+                         level, B, scale, out_xy, out_desc, out_conf, out_cap, out_count, L);        \
     return true;
 #define SFM_DQ_CASE(WS) \
   case WS:              \
@@ -545,7 +552,7 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
 
 bool launch_describe_quad(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp, int kcap,
                           const int32_t* lc, int level, double scale, int32_t* out_xy, float* out_desc,
-                          float* out_conf, int64_t out_cap, hipStream_t st) {
+                          float* out_conf, int64_t out_cap, int32_t* out_count, int L, hipStream_t st) {
   const dim3 grid((kcap + 3) / 4, B);
   switch (2 * (fw / 2)) {
     SFM_DQ_CASE(2)
@@ -566,7 +573,7 @@ bool launch_describe_quad(const float* lvl, int B, int H, int W, int fw, int rot
 #define SFM_DQ_ABL(A)                                                                                     \
   case A:                                                                                                \
     hipLaunchKernelGGL((dq::k_describe_q<18, 1, A>), grid, dim3(64), 0, st, lvl, H, W, kp, kcap, lc, level, \
-                       B, scale, out_xy, out_desc, out_conf, out_cap);                                   \
+                       B, scale, out_xy, out_desc, out_conf, out_cap, out_count, L);                     \
     return true;
           SFM_DQ_ABL(1)
           SFM_DQ_ABL(2)

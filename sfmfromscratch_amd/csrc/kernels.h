@@ -209,14 +209,18 @@ void launch_topk(const uint64_t* cand, const unsigned long long* cand_count, uin
                  MedianState* state, int mode, hipStream_t st);
 
 // describe_q.hip: four keypoints per wavefront for window widths 2..22 (false: not handled)
+// out_count (the last level's launch): also write each slot's keypoint count
 bool launch_describe_quad(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp, int kcap,
                           const int32_t* level_counts_all, int level, double scale, int32_t* out_xy,
-                          float* out_desc, float* out_conf, int64_t out_cap, hipStream_t st);
-// describe.hip: descriptors of one level written into the output slot table.
-void launch_describe(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp,
+                          float* out_desc, float* out_conf, int64_t out_cap, int32_t* out_count, int L,
+                          hipStream_t st);
+// describe.hip: descriptors of one level written into the output slot table; returns true when
+// the launch also wrote the slot counts (out_count set and the quad kernel took the level),
+// otherwise the caller runs launch_finalize_counts
+bool launch_describe(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp,
                      int kcap, const int32_t* level_counts_all, int level, int L, double scale,
                      int32_t* out_xy, float* out_desc, float* out_conf, int64_t out_cap,
-                     hipStream_t st);
+                     int32_t* out_count, hipStream_t st);
 void launch_finalize_counts(const int32_t* level_counts_all, int B, int L, int32_t* out_count,
                             hipStream_t st);
 
@@ -234,12 +238,13 @@ void launch_match_compact(const RowBest* rows, const int32_t* count, const int32
                           int* reset_counter, hipStream_t st);
 void init_match_attributes(int max_rows);
 // match_mfma.hip: exact matching with the split-fp16 MFMA prefilter
+// pmax: per-16-row-block maxima of (norm2, norm) per image, match_pmax_bytes(capP) per image
+size_t match_pmax_bytes(int64_t capP);
 void launch_match_prep(const float* desc, const int32_t* count, int nimg, int64_t cap, int64_t capP,
-                       _Float16* hi, _Float16* lo, float* norm2, float* rnorm, unsigned int* imgmax,
-                       hipStream_t st);
+                       _Float16* hi, _Float16* lo, float* norm2, float* rnorm, void* pmax, hipStream_t st);
 void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int64_t capP,
                        const _Float16* hi, const _Float16* lo, const float* norm2, const float* rnorm,
-                       const unsigned int* imgmax, const int32_t* pairs, int P, float ratio,
+                       const void* pmax, const int32_t* pairs, int P, float ratio,
                        RowBest* rows, int max_rows, uint32_t* cand, int32_t* cand_n, float* cand_thr,
                        int* ovf_count, int2* ovf_list, hipStream_t st);
 

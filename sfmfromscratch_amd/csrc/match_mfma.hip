@@ -37,72 +37,62 @@ constexpr float kScale = 256.0f;       // operand pre-scale (2^8)
 constexpr float kLoScale = 2048.0f;    // lo part scale (2^11)
 
 // Per image: fp16 hi / lo (scaled) copies, squared norms (float32 of the float64 sum),
-// norms, and per-image maxima for the error bound.
+// norms, and per-block maxima of both for the error bound (16 rows per workgroup, one wave
+// per row; the sweep reduces a pair's target-image maxima itself, so no extra launch).
+constexpr int kPrepRows = 16;
 __global__ void __launch_bounds__(256) k_match_prep(const float* __restrict__ desc,
                                                    const int32_t* __restrict__ count, int64_t cap,
                                                    int64_t capP, _Float16* __restrict__ hi,
                                                    _Float16* __restrict__ lo,
                                                    float* __restrict__ norm2,
-                                                   float* __restrict__ rnorm) {
+                                                   float* __restrict__ rnorm,
+                                                   float2* __restrict__ pmax) {
+  __shared__ float2 s_m[4];
   const int img = blockIdx.y;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);  // one wave per row
-  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n = count[img];
-  const int64_t o = ((int64_t)img * capP + row) * 128;
-  float a0 = 0.0f, a1 = 0.0f;
-  if (row < n) {
-    const float* src = desc + ((int64_t)img * cap + row) * 128;
-    a0 = src[lane];
-    a1 = src[lane + 64];
-  }
-  float v[2] = {a0, a1};
-  double s = 0.0;
+  float m2 = 0.0f, mr = 0.0f;  // this wave's rows: maxima (lane 0)
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    float x = v[q] * kScale;
-    _Float16 h = (_Float16)x;
-    float r = (x - (float)h) * kLoScale;  // exact difference, exact power-of-two scaling
-    hi[o + lane + 64 * q] = h;
-    lo[o + lane + 64 * q] = (_Float16)r;
-    s += (double)v[q] * (double)v[q];
-  }
-  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
-  if (lane == 0) {
-    float n2 = (float)s;
-    float rn = (float)sqrt(s);
-    // padding rows: +inf squared norm, so their approximate distance is +inf and the
-    // sweep needs no bounds checks (never admitted, never in the top 2)
-    norm2[(int64_t)img * capP + row] = row < n ? n2 : INFINITY;
-    rnorm[(int64_t)img * capP + row] = rn;
-  }
-}
-
-// Per-image maxima of the squared norms and norms (block reduction, no atomics).
-__global__ void __launch_bounds__(256) k_match_imgmax(const int32_t* __restrict__ count, int64_t capP,
-                                                      const float* __restrict__ norm2,
-                                                      const float* __restrict__ rnorm,
-                                                      unsigned int* __restrict__ imgmax) {
-  __shared__ float s_a[256], s_b[256];
-  const int img = blockIdx.x, tid = threadIdx.x;
-  const int n = count[img];
-  float a = 0.0f, b = 0.0f;
-  for (int r = tid; r < n; r += 256) {
-    a = fmaxf(a, norm2[(int64_t)img * capP + r]);
-    b = fmaxf(b, rnorm[(int64_t)img * capP + r]);
-  }
-  s_a[tid] = a;
-  s_b[tid] = b;
-  __syncthreads();
-  for (int off = 128; off >= 1; off >>= 1) {
-    if (tid < off) {
-      s_a[tid] = fmaxf(s_a[tid], s_a[tid + off]);
-      s_b[tid] = fmaxf(s_b[tid], s_b[tid + off]);
+  for (int k = 0; k < kPrepRows / 4; ++k) {
+    const int row = blockIdx.x * kPrepRows + wv * (kPrepRows / 4) + k;
+    const int64_t o = ((int64_t)img * capP + row) * 128;
+    float a0 = 0.0f, a1 = 0.0f;
+    if (row < n) {
+      const float* src = desc + ((int64_t)img * cap + row) * 128;
+      a0 = src[lane];
+      a1 = src[lane + 64];
     }
-    __syncthreads();
+    float v[2] = {a0, a1};
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float x = v[q] * kScale;
+      _Float16 h = (_Float16)x;
+      float r = (x - (float)h) * kLoScale;  // exact difference, exact power-of-two scaling
+      hi[o + lane + 64 * q] = h;
+      lo[o + lane + 64 * q] = (_Float16)r;
+      s += (double)v[q] * (double)v[q];
+    }
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+    if (lane == 0) {
+      float n2 = (float)s;
+      float rn = (float)sqrt(s);
+      // padding rows: +inf squared norm, so their approximate distance is +inf and the
+      // sweep needs no bounds checks (never admitted, never in the top 2)
+      norm2[(int64_t)img * capP + row] = row < n ? n2 : INFINITY;
+      rnorm[(int64_t)img * capP + row] = rn;
+      if (row < n) {
+        m2 = fmaxf(m2, n2);
+        mr = fmaxf(mr, rn);
+      }
+    }
   }
-  if (tid == 0) {
-    imgmax[img * 2 + 0] = __float_as_uint(s_a[0]);
-    imgmax[img * 2 + 1] = __float_as_uint(s_b[0]);
+  if (lane == 0) s_m[wv] = make_float2(m2, mr);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float2 r = s_m[0];
+    for (int w = 1; w < 4; ++w) r = make_float2(fmaxf(r.x, s_m[w].x), fmaxf(r.y, s_m[w].y));
+    pmax[(int64_t)img * gridDim.x + blockIdx.x] = r;
   }
 }
 
@@ -186,7 +176,7 @@ template <int ABL>
 __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
     const int32_t* __restrict__ count, int64_t capP, const _Float16* __restrict__ hi,
     const _Float16* __restrict__ lo, const float* __restrict__ norm2, const float* __restrict__ rnorm,
-    const unsigned int* __restrict__ imgmax, const int32_t* __restrict__ pairs, int P, int max_rows,
+    const float2* __restrict__ pmax, const int32_t* __restrict__ pairs, int P, int max_rows,
     uint32_t* __restrict__ cand, int32_t* __restrict__ cand_n, float* __restrict__ cand_thr,
     int* __restrict__ ovf_count, int2* __restrict__ ovf_list) {
   // stage buffers: stage st in sT[st & 1] (hi, lo); its target norms in sN[st % 3] (the carried
@@ -221,8 +211,35 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   }
   const float na = norm2[(int64_t)i1 * capP + qi];
   const float ra = rnorm[(int64_t)i1 * capP + qi];
-  const float maxn2 = __uint_as_float(imgmax[i2 * 2 + 0]);
-  const float maxrn = __uint_as_float(imgmax[i2 * 2 + 1]);
+  // the target image's maxima of norm2 / norm: reduced here from k_match_prep's per-block
+  // maxima (capP / kPrepRows of them), through sD before its first use
+  float maxn2, maxrn;
+  {
+    const int nblk = (int)(capP / kPrepRows);
+    float m2 = 0.0f, mr = 0.0f;
+    for (int t = tid; t < nblk; t += kNT) {
+      const float2 v = pmax[(int64_t)i2 * nblk + t];
+      m2 = fmaxf(m2, v.x);
+      mr = fmaxf(mr, v.y);
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+      m2 = fmaxf(m2, __shfl_xor(m2, off));
+      mr = fmaxf(mr, __shfl_xor(mr, off));
+    }
+    float* red = &sD[0][0][0];
+    if (lane == 0) {
+      red[2 * wid] = m2;
+      red[2 * wid + 1] = mr;
+    }
+    __syncthreads();
+    maxn2 = red[0];
+    maxrn = red[1];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) {
+      maxn2 = fmaxf(maxn2, red[2 * w]);
+      maxrn = fmaxf(maxrn, red[2 * w + 1]);
+    }
+  }
   // rigorous |d~ - d_ref| bound (matcher exactness)
   const float E = 3.0517578125e-05f * ra * maxrn + 4e-6f * (na + maxn2) + 1.25e-4f;
   const float E2 = 2.0f * E;
@@ -701,17 +718,17 @@ __global__ void __launch_bounds__(256) k_match_overflow(const float* __restrict_
   }
 }
 
+size_t match_pmax_bytes(int64_t capP) { return (size_t)(capP / kPrepRows) * sizeof(float2); }
+
 void launch_match_prep(const float* desc, const int32_t* count, int nimg, int64_t cap, int64_t capP,
-                       _Float16* hi, _Float16* lo, float* norm2, float* rnorm, unsigned int* imgmax,
-                       hipStream_t st) {
-  hipLaunchKernelGGL(k_match_prep, dim3((unsigned)(capP / 4), nimg), dim3(256), 0, st, desc, count, cap, capP, hi,
-                     lo, norm2, rnorm);
-  hipLaunchKernelGGL(k_match_imgmax, dim3(nimg), dim3(256), 0, st, count, capP, norm2, rnorm, imgmax);
+                       _Float16* hi, _Float16* lo, float* norm2, float* rnorm, void* pmax, hipStream_t st) {
+  hipLaunchKernelGGL(k_match_prep, dim3((unsigned)(capP / kPrepRows), nimg), dim3(256), 0, st, desc, count, cap,
+                     capP, hi, lo, norm2, rnorm, static_cast<float2*>(pmax));
 }
 
 void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int64_t capP,
                        const _Float16* hi, const _Float16* lo, const float* norm2, const float* rnorm,
-                       const unsigned int* imgmax, const int32_t* pairs, int P, float ratio,
+                       const void* pmax, const int32_t* pairs, int P, float ratio,
                        RowBest* rows, int max_rows, uint32_t* cand, int32_t* cand_n, float* cand_thr,
                        int* ovf_count, int2* ovf_list, hipStream_t st) {
   static const int abl = [] {
@@ -726,7 +743,8 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
   const dim3 grid((unsigned)(8 * ((P + 7) / 8) * qb));
   // ovf_count is zero here: set once at allocation, re-zeroed by k_match_compact
 #define SFM_SWEEP(A)                                                                                           \
-  hipLaunchKernelGGL(k_match_mfma<A>, grid, dim3(kNT), 0, st, count, capP, hi, lo, norm2, rnorm, imgmax, pairs, P, \
+  hipLaunchKernelGGL(k_match_mfma<A>, grid, dim3(kNT), 0, st, count, capP, hi, lo, norm2, rnorm,                 \
+                     static_cast<const float2*>(pmax), pairs, P,                                                  \
                      max_rows, cand, cand_n, cand_thr, ovf_count, ovf_list)
   if (abl == 9)
     SFM_SWEEP(9);

@@ -354,10 +354,13 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     launch_topk(e.cand, candcnt2 + e.co, as<uint64_t>(c->d_scratch) + (l < L_aux ? 0 : (int64_t)B * H * W), e.kp,
                 std::max(c->kcap, 1), c->kcap, B, h, w, lv[l].fw / 2, e.med, 1, s);
   };
+  bool counted = false;  // the last level's describe launch wrote the slot counts
   auto describe_level = [&](int l, hipStream_t s) {
     StageScope sc(c, SFM_PROF_DESCRIBE, s);
-    launch_describe(lvl[l], B, lv[l].h, lv[l].w, lv[l].fw, rotate, lb[l].kp, c->kcap, as<int32_t>(c->d_lc), l, L,
-                    lv[l].scale, xy, desc, conf, cap, s);
+    const bool r = launch_describe(lvl[l], B, lv[l].h, lv[l].w, lv[l].fw, rotate, lb[l].kp, c->kcap,
+                                   as<int32_t>(c->d_lc), l, L, lv[l].scale, xy, desc, conf, cap,
+                                   l == L - 1 ? count : nullptr, s);
+    if (l == L - 1) counted = r;
   };
   // Harris launches: one per level, unless SFMFEAT_HARRIS_GROUP=g (g >= 1): levels >= g then
   // share launches (up to kHarrisMaxLevels each).  Off by default: grouping L1-L3 or L2-L3 cut
@@ -407,7 +410,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   // join: the caller's stream waits for the aux work
   HIPCHK(c, hipEventRecord(c->ev[L + 1], ax));
   HIPCHK(c, hipStreamWaitEvent(st, c->ev[L + 1], 0));
-  launch_finalize_counts(as<int32_t>(c->d_lc), B, L, count, st);
+  if (!counted) launch_finalize_counts(as<int32_t>(c->d_lc), B, L, count, st);
   HIPCHK(c, hipGetLastError());
   return SFM_OK;
 }
@@ -437,13 +440,13 @@ int match_prep_range(sfm_ctx* c, const float* desc, const int32_t* count, int ni
     if ((rc = ensure(c, c->m_lo, (size_t)nimg * capP * 128 * 2))) return rc;
     if ((rc = ensure(c, c->m_norm2, (size_t)nimg * capP * 4))) return rc;
     if ((rc = ensure(c, c->m_rnorm, (size_t)nimg * capP * 4))) return rc;
-    if ((rc = ensure(c, c->m_imgmax, (size_t)nimg * 8))) return rc;
+    if ((rc = ensure(c, c->m_imgmax, (size_t)nimg * match_pmax_bytes(capP)))) return rc;
     if (n == 0) return SFM_OK;
     StageScope sc(c, SFM_PROF_MATCH_PREP, st);
     const int64_t o = (int64_t)lo * capP;
     launch_match_prep(d0, count + lo, n, cap, capP, as<_Float16>(c->m_hi) + o * 128, as<_Float16>(c->m_lo) + o * 128,
-                      as<float>(c->m_norm2) + o, as<float>(c->m_rnorm) + o, as<unsigned int>(c->m_imgmax) + 2 * lo,
-                      st);
+                      as<float>(c->m_norm2) + o, as<float>(c->m_rnorm) + o,
+                      as<char>(c->m_imgmax) + (size_t)lo * match_pmax_bytes(capP), st);
   }
   HIPCHK(c, hipGetLastError());
   return SFM_OK;
@@ -494,7 +497,7 @@ int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, in
       const int64_t capP = (cap + 127) / 128 * 128;
       StageScope sc(c, SFM_PROF_MATCH, st);
       launch_match_mfma(desc, count, cap, capP, as<_Float16>(c->m_hi), as<_Float16>(c->m_lo), as<float>(c->m_norm2),
-                        as<float>(c->m_rnorm), as<unsigned int>(c->m_imgmax), pr, Pn, ratio, as<RowBest>(c->m_rows),
+                        as<float>(c->m_rnorm), c->m_imgmax.p, pr, Pn, ratio, as<RowBest>(c->m_rows),
                         (int)cap, as<uint32_t>(c->m_cand), as<int32_t>(c->m_candn), as<float>(c->m_candt),
                         as<int>(c->m_ovfc), as<int2>(c->m_ovf), st);
     }
