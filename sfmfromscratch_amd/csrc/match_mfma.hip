@@ -143,47 +143,83 @@ SFM_DEV void top2_merge(float& b1, int& j1, float& b2, float ob1, int oj1, float
 }
 
 constexpr int kTT2 = 64;               // targets per LDS stage (two 32-target MFMA sub-tiles)
-constexpr int kStageHalves = kTT2 * kRowH;  // f16 elements per array per stage
-// LDS of one sweep workgroup: two stage buffers (hi, lo) + target norms (three stages) + the
-// per-wave d~ staging of the appends.  Over 160 KB - sizeof(k_harris's LDS) on purpose: a sweep
-// workgroup then never shares a CU with a Harris workgroup of a concurrent extraction (two
-// streams).  On gfx950 that pairing corrupted ~0.3 % of k_harris's v_pk_fma_f32 results
-// (tools/check_c4b.py; the inputs verified unchanged inside the kernel), so the exclusion is by
-// construction, and one 512-thread workgroup per CU keeps two waves per SIMD.
-constexpr size_t kSweepLds = 2 * 2 * kStageHalves * 2 + 3 * kTT2 * 4 + kWaves * 64 * 16 * 4;
+// LDS of one sweep workgroup (one __shared__ array; carved per staging form below): stage
+// buffers (hi, lo), target norms of the stages in use, the per-wave d~ staging of the appends.
+// Over 160 KB - sizeof(k_harris's LDS) on purpose: a sweep workgroup then never shares a CU
+// with a Harris workgroup of a concurrent extraction (two streams).  On gfx950 that pairing
+// corrupted ~0.3 % of k_harris's v_pk_fma_f32 results (tools/check_c4b.py; the kernel's
+// inputs verified unchanged inside it), so the exclusion is by construction, and one
+// 512-thread workgroup per CU keeps two waves per SIMD.
+constexpr int kDmaBufs = 3, kDmaNormBufs = 4;  // LDS-DMA staging: stage s + 2 in flight over s
+constexpr int kRegBufs = 2, kRegNormBufs = 3;  // register staging
+constexpr size_t kDBytes = (size_t)kWaves * 64 * 16 * 4;  // per-wave d~ staging of the appends
+constexpr size_t kSweepLds = (size_t)kDmaBufs * 2 * kTT2 * 256 + kDmaNormBufs * kTT2 * 4 + kDBytes;
+static_assert(kSweepLds >= (size_t)kRegBufs * 2 * kTT2 * kRowH * 2 + kRegNormBufs * kTT2 * 4 + kDBytes,
+              "one LDS array serves both staging forms");
 static_assert(kSweepLds > 160 * 1024 - 71720, "a sweep workgroup must not fit beside a k_harris workgroup");
+static_assert(kSweepLds <= 160 * 1024, "LDS per CU");
 
-// One workgroup = 4 waves x 32 query rows; ONE sweep over the target table of the pair in
-// 64-row LDS stages (the next stage's hi/lo rows are loaded into registers while the
-// current stage's MFMAs run, then stored into the single LDS stage buffer), software-
-// pipelined by 32-target sub-tile: the MFMAs of one sub-tile run beside the epilogue of
-// the previous one.  Per element the epilogue forms d~, updates the row's running top-2
-// (two v_med3) and admits the target when d~ <= thr, thr = b2~(so far) + 2E: this lane's
-// own b2~ after the sub-tile, capped by the wave-merged b2~ of the previous stage.  b2~
-// only decreases, so every running thr >= the final one and the admitted set contains
-// the row's final window (argument below).  thr uses the row's b2~ over both half-waves
-// (merged after every sub-tile).  Admitted target indices go to the row's list in global
-// memory: each half-wave lane appends to its own kHalfCap entries with a register count
-// (no LDS atomics), and the row's count word holds both (low / high 16 bits);
-// k_match_rerank recomputes them with the reference's exact float32 distance; a row
-// whose list overflowed goes to k_match_overflow (exact over all targets).
+// LDS-DMA (global_load_lds) issued from inline asm, M0 = the wave-uniform LDS destination:
+// hipcc's own waitcnt pass then does not see them (it would wait vmcnt(0) ahead of every LDS
+// read while one is in flight, draining the prefetch); the sweep counts them itself
+__device__ __forceinline__ void glds_x4(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+__device__ __forceinline__ void glds_x1(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
+// One workgroup = 8 waves x 32 query rows; ONE sweep over the target table of the pair in
+// 64-row LDS stages, software-pipelined by 32-target sub-tile: the MFMAs of one sub-tile run
+// beside the epilogue of the previous one.  Staging (STAGE):
+//   1 (default): LDS-DMA.  Each wave issues its share of a stage as global_load_lds_dwordx4
+//     (1 KB = 4 target rows per instruction, no VGPRs, no ds_write); rows are 256 B with the
+//     16-B pieces XOR-swizzled by row (the swizzle is on the per-lane SOURCE address: the DMA
+//     destination is lane-linear) so the fragment reads are conflict-free.  Three buffers:
+//     stage s + 2 is issued at the end of iteration s and stays in flight across the next
+//     barrier (counted vmcnt, raw s_barrier); the appends' stores come before it in issue
+//     order, so the count stays static.
+//   0: register staging (global -> VGPRs -> ds_write into padded rows), two buffers (A/B).
+// Per element the epilogue forms d~, updates the row's running top-2 (two v_med3) and admits
+// the target when d~ <= thr, thr = b2~(so far) + 2E: this lane's own b2~ after the sub-tile,
+// capped by the wave-merged b2~ of the previous stage.  b2~ only decreases, so every running
+// thr >= the final one and the admitted set contains the row's final window (argument
+// below).  thr uses the row's b2~ over both half-waves (merged after every sub-tile).
+// Admitted target indices go to the row's list in global memory: each half-wave lane appends
+// to its own kHalfCap entries with a register count (no LDS atomics), and the row's count
+// word holds both (low / high 16 bits); k_match_rerank recomputes them with the reference's
+// exact float32 distance; a row whose list overflowed goes to k_match_overflow (exact over
+// all targets).
 // The window argument: the targets achieving b1~ and b2~ have exact distances <= b1~ + E and
 // <= b2~ + E, so the exact second-smallest D2 <= b2~ + E; a target with exact d <= D2 has
 // d~ <= d + E <= b2~ + 2E.  Targets outside the window are strictly farther than D2.
-// ABL (timing builds only; results are wrong unless 0): 9 = no epilogue, 10 = no MFMAs,
-// 11 = no stage loads (every stage reuses stage 0's LDS rows), 12 = no list appends
-template <int ABL>
+template <int STAGE>
 __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
     const int32_t* __restrict__ count, int64_t capP, const _Float16* __restrict__ hi,
     const _Float16* __restrict__ lo, const float* __restrict__ norm2, const float* __restrict__ rnorm,
     const float2* __restrict__ pmax, const int32_t* __restrict__ pairs, int P, int max_rows,
     uint32_t* __restrict__ cand, int32_t* __restrict__ cand_n, float* __restrict__ cand_thr,
     int* __restrict__ ovf_count, int2* __restrict__ ovf_list) {
-  // stage buffers: stage st in sT[st & 1] (hi, lo); its target norms in sN[st % 3] (the carried
-  // sub-tile's epilogue reads stage st - 1's norms while stage st + 1's are being stored)
-  __shared__ __attribute__((aligned(16))) _Float16 sT[2][2][kStageHalves];
-  __shared__ __attribute__((aligned(16))) float sN[3][kTT2];
-  __shared__ __attribute__((aligned(16))) float sD[kWaves][64][16];  // a sub-tile's d~ per lane
+  constexpr bool DMA = STAGE == 1;
+  constexpr int NBUF = DMA ? kDmaBufs : kRegBufs;
+  constexpr int NNB = DMA ? kDmaNormBufs : kRegNormBufs;
+  constexpr int ROWB = DMA ? 256 : kRowH * 2;  // bytes per staged target row
+  constexpr int ARRB = kTT2 * ROWB;            // one array (hi or lo) of a stage
+  constexpr int BUFB = 2 * ARRB;
+  constexpr int OFF_N = NBUF * BUFB;
+  constexpr int OFF_D = OFF_N + NNB * kTT2 * 4;
+  static_assert((size_t)OFF_D + kDBytes <= kSweepLds, "LDS carve");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kSweepLds];
+  float* const sNb = reinterpret_cast<float*>(smem + OFF_N);  // [NNB][kTT2]
+  float* const sDb = reinterpret_cast<float*>(smem + OFF_D);  // [kWaves][64][16]
 
   // XCD-aware mapping (workgroups b and b + 8 share an XCD and its L2): group g = b % 8
   // takes the pairs p = g (mod 8), so all query blocks of a pair stream its target table
@@ -199,7 +235,7 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   if (row0 >= n1 || n2 < 1) return;
 
   // this lane's query row (column of the MFMA output) and its fragments, kept in registers
-  const int ql = wid * kQW + (lane & 31);           // local query row 0..127
+  const int ql = wid * kQW + (lane & 31);           // local query row 0..255
   const int qi = row0 + ql;                          // query row in image i1
   const int half = lane >> 5;
   const int64_t qo = ((int64_t)i1 * capP + qi) * 128;
@@ -212,7 +248,7 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   const float na = norm2[(int64_t)i1 * capP + qi];
   const float ra = rnorm[(int64_t)i1 * capP + qi];
   // the target image's maxima of norm2 / norm: reduced here from k_match_prep's per-block
-  // maxima (capP / kPrepRows of them), through sD before its first use
+  // maxima (capP / kPrepRows of them), through the d~ staging area before its first use
   float maxn2, maxrn;
   {
     const int nblk = (int)(capP / kPrepRows);
@@ -226,19 +262,19 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
       m2 = fmaxf(m2, __shfl_xor(m2, off));
       mr = fmaxf(mr, __shfl_xor(mr, off));
     }
-    float* red = &sD[0][0][0];
     if (lane == 0) {
-      red[2 * wid] = m2;
-      red[2 * wid + 1] = mr;
+      sDb[2 * wid] = m2;
+      sDb[2 * wid + 1] = mr;
     }
     __syncthreads();
-    maxn2 = red[0];
-    maxrn = red[1];
+    maxn2 = sDb[0];
+    maxrn = sDb[1];
 #pragma unroll
     for (int w = 1; w < kWaves; ++w) {
-      maxn2 = fmaxf(maxn2, red[2 * w]);
-      maxrn = fmaxf(maxrn, red[2 * w + 1]);
+      maxn2 = fmaxf(maxn2, sDb[2 * w]);
+      maxrn = fmaxf(maxrn, sDb[2 * w + 1]);
     }
+    __syncthreads();  // the d~ staging area is free again
   }
   // rigorous |d~ - d_ref| bound (matcher exactness)
   const float E = 3.0517578125e-05f * ra * maxrn + 4e-6f * (na + maxn2) + 1.25e-4f;
@@ -249,53 +285,88 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
 
   const int nst = (n2 + kTT2 - 1) / kTT2;
   const int64_t to = (int64_t)i2 * capP * 128;
-  // stage loader: 64 rows x (hi, lo) x 256 B = 32 KB, each array one contiguous 16 KB run;
-  // pass q reads 8 KB of it with consecutive 16-B pieces per lane (one 1 KB run per wave
-  // instruction): thread t -> row 32 q + t / 16, halves 8 (t % 16)
+  const float* const nrm_t = norm2 + (int64_t)i2 * capP;
+
+  // ---- LDS-DMA staging (STAGE 1): wave w fetches chunks w and w + 8 (4 rows each) of both
+  //      arrays; lane l of a chunk: row 4 ci + l / 16, LDS piece l % 16 = global piece
+  //      (l % 16) ^ (row % 16).  Wave 0 also fetches the stage's 64 target norms.
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  const uint32_t smem_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) unsigned char*)smem);
+  auto issue_stage = [&](int stg, int buf, int nbuf) {
+    const int64_t rb = (int64_t)stg * kTT2;  // rows < capP: in bounds
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int a = j >> 1, ci = (j & 1) * 8 + wid;
+      const int ciu = (j & 1) * 8 + wid_u;
+      const int row = 4 * ci + (lane >> 4);
+      const int c = (lane & 15) ^ (row & 15);
+      const _Float16* src = (a ? lo : hi) + to + (rb + row) * 128 + c * 8;
+      glds_x4(src, smem_lds + (uint32_t)(buf * BUFB + a * ARRB + ciu * 1024));
+    }
+    if (wid_u == 0) glds_x1(nrm_t + rb + lane, smem_lds + (uint32_t)(OFF_N + nbuf * kTT2 * 4));
+  };
+  // this wave's share of the stage issued two iterations ago has landed (the last stage's
+  // share stays in flight); then every wave's
+  auto stage_barrier = [&]() {
+    if constexpr (DMA) {
+      if (wid_u == 0) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();
+    }
+  };
+
+  // ---- register staging (STAGE 0): thread t -> row 32 q + t / 16, halves 8 (t % 16)
   const int lr = tid >> 4, lc = (tid & 15) * 8;
-  h8 g[4];
+  h8 g[DMA ? 1 : 4];
   auto load_stage = [&](int st) {
-    if (ABL == 11 && st > 0) return;
-    const int64_t gofs = to + (int64_t)(st * kTT2) * 128 + tid * 8;  // rows < capP: in bounds
+    if constexpr (!DMA) {
+      const int64_t gofs = to + (int64_t)(st * kTT2) * 128 + tid * 8;  // rows < capP: in bounds
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      g[q] = *reinterpret_cast<const h8*>(hi + gofs + 4096 * q);
-      g[2 + q] = *reinterpret_cast<const h8*>(lo + gofs + 4096 * q);
+      for (int q = 0; q < 2; ++q) {
+        g[q] = *reinterpret_cast<const h8*>(hi + gofs + 4096 * q);
+        g[2 + q] = *reinterpret_cast<const h8*>(lo + gofs + 4096 * q);
+      }
     }
   };
-  auto store_stage = [&](int buf, bool first) {
-    if (ABL == 11 && !first) return;
+  auto store_stage = [&](int buf) {
+    if constexpr (!DMA) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      *reinterpret_cast<h8*>(&sT[buf][0][(32 * q + lr) * kRowH + lc]) = g[q];
-      *reinterpret_cast<h8*>(&sT[buf][1][(32 * q + lr) * kRowH + lc]) = g[2 + q];
+      for (int q = 0; q < 2; ++q) {
+        *reinterpret_cast<h8*>(smem + buf * BUFB + ((32 * q + lr) * kRowH + lc) * 2) = g[q];
+        *reinterpret_cast<h8*>(smem + buf * BUFB + ARRB + ((32 * q + lr) * kRowH + lc) * 2) = g[2 + q];
+      }
     }
   };
-  // 32 targets x 32 queries of sub-tile `sub` of the stage in buffer `buf`: hi.hi into ahh,
-  // hi.lo + lo.hi into ax (one accumulation chain each)
-  auto mfma_sub = [&](int buf, int sub, f32x16& ahh, f32x16& ax) {
-    const _Float16* tH = &sT[buf][0][0];
-    const _Float16* tL = &sT[buf][1][0];
-    const int trow = (32 * sub + (lane & 31)) * kRowH;
+
+  // fragment byte offsets of k-step kk inside a stage buffer (sub-tile 0, hi array)
+  int frag[8];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    if constexpr (DMA) frag[kk] = (lane & 31) * 256 + (((2 * kk + half) ^ (lane & 15)) << 4);
+    else frag[kk] = ((lane & 31) * kRowH + kk * 16 + 8 * half) * 2;
+  }
+  // 32 targets x 32 queries of sub-tile `sub` of the stage at byte offset `bofs`: hi.hi into
+  // ahh, hi.lo + lo.hi into ax (one accumulation chain each)
+  auto mfma_sub = [&](const int (&vb)[8], int sub, f32x16& ahh, f32x16& ax) {
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-      const int ko = kk * 16 + 8 * half;
-      const h8 thi = *reinterpret_cast<const h8*>(tH + trow + ko);
-      const h8 tlo = *reinterpret_cast<const h8*>(tL + trow + ko);
-      if (ABL == 10) {
-        asm volatile("" ::"v"(thi), "v"(tlo));
-        continue;
-      }
-      ahh = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qhi[kk], ahh, 0, 0, 0);
-      ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qlo[kk], ax, 0, 0, 0);
+      const h8 thi = *reinterpret_cast<const h8*>(smem + vb[kk] + sub * 32 * ROWB);
+      const h8 tlo = *reinterpret_cast<const h8*>(smem + vb[kk] + sub * 32 * ROWB + ARRB);
+      // k-step 0 starts both chains from an inline-constant zero accumulator
+      ahh = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qhi[kk], kk == 0 ? f32x16{} : ahh, 0, 0, 0);
+      ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qlo[kk], kk == 0 ? f32x16{} : ax, 0, 0, 0);
       ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(tlo, qhi[kk], ax, 0, 0, 0);
     }
   };
   // this lane's 16 target norms of sub-tile `sub` (MFMA row layout: 8 (rr >> 2) + 4 half + (rr & 3))
-  auto load_nb = [&](int par, int sub, float (&nb)[16]) {
+  auto load_nb = [&](int nbuf, int sub, float (&nb)[16]) {
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const float4 v = *reinterpret_cast<const float4*>(&sN[par][32 * sub + 8 * g4 + 4 * half]);
+      const float4 v = *reinterpret_cast<const float4*>(sNb + nbuf * kTT2 + 32 * sub + 8 * g4 + 4 * half);
       nb[4 * g4 + 0] = v.x; nb[4 * g4 + 1] = v.y; nb[4 * g4 + 2] = v.z; nb[4 * g4 + 3] = v.w;
     }
   };
@@ -306,23 +377,40 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   // (each rounding is covered by E's 4e-6 (na + nb) term); padding targets
   // have norm2 = +inf: d~ = +inf.  Running top-2 (b2 = med3(b1, b2, d), b1 = min), then
   // bit rr of mm for d~ <= min(b2~ + 2E, thr_w)
+  // The sub-tile's two smallest d~ by a tournament (pairs (min, max), then merges
+  // m = min(ma, mb), s = min3(max(ma, mb), sa, sb)): the same multiset top-2 as an element-by-
+  // element update, at a dependency depth of 9 instead of 32; merged into the running
+  // (b1, b2) the same way.  The admission mask is built only when some lane's smallest d~
+  // passes the threshold (after the first stages, most sub-tiles admit nothing).
   auto epi = [&](const f32x16& ahh, const f32x16& ax, const float (&nb)[16], float (&d)[16], uint32_t& mm) {
-    if (ABL == 9) {
-      asm volatile("" ::"v"(ahh), "v"(ax));
-      return;
-    }
 #pragma unroll
-    for (int rr = 0; rr < 16; ++rr) {
+    for (int rr = 0; rr < 16; ++rr)
       d[rr] = __builtin_fmaf(ax[rr], -1.4901161193847656e-08f /* -2^-26 */,
                              __builtin_fmaf(ahh[rr], -3.0517578125e-05f /* -2^-15 */, na + nb[rr]));
-      b2 = __builtin_amdgcn_fmed3f(b1, b2, d[rr]);
-      b1 = __builtin_amdgcn_fmed3f(b1, d[rr], -INFINITY);
+    float m[8], sc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      m[i] = fminf(d[2 * i], d[2 * i + 1]);
+      sc[i] = fmaxf(d[2 * i], d[2 * i + 1]);
     }
+#pragma unroll
+    for (int w = 4; w >= 1; w >>= 1)
+#pragma unroll
+      for (int i = 0; i < w; ++i) {
+        const float mm0 = fminf(m[i], m[i + w]);
+        sc[i] = fminf(fmaxf(m[i], m[i + w]), fminf(sc[i], sc[i + w]));
+        m[i] = mm0;
+      }
+    const float tm = m[0];
+    b2 = fminf(fmaxf(b1, tm), fminf(b2, sc[0]));
+    b1 = fminf(b1, tm);
     // the row's b2~ so far over both halves (every lane's b2 and b1 >= its half's final ones)
     const float ob1 = other_half(b1), ob2 = other_half(b2);
     const float t = fminf(fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + E2, thr_w);
+    if (__any(tm <= t)) {
 #pragma unroll
-    for (int rr = 0; rr < 16; ++rr) mm |= (d[rr] <= t) ? (1u << rr) : 0u;
+      for (int rr = 0; rr < 16; ++rr) mm |= (d[rr] <= t) ? (1u << rr) : 0u;
+    }
   };
   // MFMA / VALU interleave of one software-pipelined region: the three MFMAs of a k-step
   // with the epilogue's vector instructions in their gaps
@@ -348,12 +436,8 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   // (rr & 3)) -> the row's global list as (index | d~ rounded down to bf16 << 16).  When
   // any lane of the wave admits, the lane's 16 d~ go to its LDS row (4 x 16-B stores) and
   // each admitted one is read back by index (no dynamic register indexing into d)
-  float* my_d = &sD[wid][lane][0];
+  float* my_d = sDb + (wid * 64 + lane) * 16;
   auto append = [&](uint32_t mm, const float (&d)[16], int jb) {
-    if (ABL == 12) {
-      asm volatile("" ::"v"(mm));
-      return;
-    }
     if (__any(mm != 0u)) {  // wave-uniform: skip when no lane admits
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -368,75 +452,94 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
     }
   };
 
-  load_stage(0);
-  const float nrm_t0 = (tid < kTT2) ? norm2[(int64_t)i2 * capP + tid] : 0.0f;
-  store_stage(0, true);
-  if (tid < kTT2) {
-    sN[0][tid] = nrm_t0;
-    sN[2][tid] = INFINITY;  // "stage -1": the carried sub-tile's first epilogue is a no-op
+  // prologue: stages 0 and 1 (DMA) / stage 0 (registers); "stage -1"'s norms are +inf, so
+  // the carried sub-tile's first epilogue is a no-op
+  if constexpr (DMA) {
+    // the query fragments are in registers before the first DMA is issued: hipcc's wait for
+    // them would otherwise be a vmcnt(0) that drains the prologue's prefetch too
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) asm volatile("" ::"v"(qhi[kk]), "v"(qlo[kk]));
+    asm volatile("" ::"v"(E2), "v"(na));
+    issue_stage(0, 0, 0);
+    issue_stage(min(1, nst - 1), 1, 1);
+    if (wid_u == 0) sNb[(NNB - 1) * kTT2 + lane] = INFINITY;
+  } else {
+    load_stage(0);
+    const float nrm_t0 = (tid < kTT2) ? nrm_t[tid] : 0.0f;
+    store_stage(0);
+    if (tid < kTT2) {
+      sNb[tid] = nrm_t0;
+      sNb[(NNB - 1) * kTT2 + tid] = INFINITY;
+    }
   }
-  f32x16 ph_hh = {}, ph_x = {};  // carried sub-tile 1 of the previous stage
-  int n3 = 0;                    // st % 3
+  // accumulators: set A = sub-tile 0 of a stage, set B = sub-tile 1 (carried into the next
+  // iteration's first region); alternating sets instead of copies
+  f32x16 hA = {}, xA = {}, hB = {}, xB = {};
+  int nbc = 0;                   // norm buffer of stage st (st % NNB)
+  int buf = 0;                   // stage buffer of stage st (st % NBUF)
   for (int st = 0; st < nst; ++st) {
-    // stage st (buffer st & 1) is visible, and every wave is done with stage st - 1's rows,
-    // so its buffer takes stage st + 1 below: one barrier per stage
-    __syncthreads();
-    // next stage's rows (the last stage re-reads itself: branch-free loop body, so the
-    // MFMAs and the epilogue share one scheduling region)
-    const int sn = min(st + 1, nst - 1);
-    load_stage(sn);
-    const float nrm_next = norm2[(int64_t)i2 * capP + sn * kTT2 + (tid & (kTT2 - 1))];
-    const int buf = st & 1;
-    const int np3 = n3 == 0 ? 2 : n3 - 1, nn3 = n3 == 2 ? 0 : n3 + 1;
+    // stage st is visible, and every wave is done with stage st - 1 (DMA: st - 1's buffer
+    // takes stage st + 2 at the end of this iteration; registers: stage st + 1): one barrier
+    stage_barrier();
+    const int nbp = nbc == 0 ? NNB - 1 : nbc - 1, nbn = nbc == NNB - 1 ? 0 : nbc + 1;
+    float nrm_next = 0.0f;
+    if constexpr (!DMA) {  // next stage's rows (the last stage re-reads itself: branch-free body)
+      const int sn = min(st + 1, nst - 1);
+      load_stage(sn);
+      nrm_next = nrm_t[sn * kTT2 + (tid & (kTT2 - 1))];
+    }
+    int vb[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) vb[kk] = frag[kk] + buf * BUFB;
     {
       float nb[16], d[16];
       uint32_t mm = 0;
-      f32x16 h0 = {}, x0 = {};
-      load_nb(np3, 1, nb);
-      mfma_sub(buf, 0, h0, x0);
-      epi(ph_hh, ph_x, nb, d, mm);
+      load_nb(nbp, 1, nb);
+      mfma_sub(vb, 0, hA, xA);
+      epi(hB, xB, nb, d, mm);
       interleave();
       pin(b1, b2, mm);
       append(mm, d, (st - 1) * kTT2 + 32);
-      ph_hh = h0;
-      ph_x = x0;
     }
     {
       float nb[16], d[16];
       uint32_t mm = 0;
-      f32x16 h1 = {}, x1 = {};
-      load_nb(n3, 0, nb);
-      mfma_sub(buf, 1, h1, x1);
-      epi(ph_hh, ph_x, nb, d, mm);
+      load_nb(nbc, 0, nb);
+      mfma_sub(vb, 1, hB, xB);
+      epi(hA, xA, nb, d, mm);
       interleave();
       pin(b1, b2, mm);
       append(mm, d, st * kTT2);
-      ph_hh = h1;
-      ph_x = x1;
     }
     {  // the wave-merged running threshold for the next stage (both halves of a row)
       const float ob1 = other_half(b1), ob2 = other_half(b2);
       thr_w = fminf(fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + E2, thr_w);
     }
-    store_stage(buf ^ 1, false);
-    if (tid < kTT2) sN[nn3][tid] = nrm_next;
-    n3 = nn3;
+    if constexpr (DMA) {
+      // stage st + 2 into stage st - 1's buffer, after this iteration's appends in issue
+      // order (the counted wait above leaves exactly these in flight)
+      const int b2i = buf == 0 ? 2 : buf - 1;
+      const int n2i = nbn == NNB - 1 ? 0 : nbn + 1;
+      issue_stage(min(st + 2, nst - 1), b2i, n2i);
+    } else {
+      store_stage(buf ^ 1);
+      if (tid < kTT2) sNb[nbn * kTT2 + tid] = nrm_next;
+    }
+    nbc = nbn;
+    buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
   {
     uint32_t mm = 0;  // the last stage's sub-tile 1 (its norms: stage nst - 1)
     float nb[16], d[16];
-    load_nb(n3 == 0 ? 2 : n3 - 1, 1, nb);
-    epi(ph_hh, ph_x, nb, d, mm);
+    load_nb(nbc == 0 ? NNB - 1 : nbc - 1, 1, nb);
+    epi(hB, xB, nb, d, mm);
     append(mm, d, (nst - 1) * kTT2 + 32);
   }
+  if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA in flight at exit
   // the row's final window threshold (both halves merged): the re-rank drops the admitted
   // targets above it (their stored d~ is rounded down, so no window member is dropped)
   const float ob1 = other_half(b1), ob2 = other_half(b2);
   const float thr_final = fminf(fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + E2, thr_w);
-  if (ABL != 0) {
-    if (thr_final == -1.0f) cand_n[0] = 1;  // defeats dead-code elimination
-    return;
-  }
   const int ocnt = other_half(cnt);
   if (live && half == 0) {
     cand_thr[(int64_t)p * max_rows + qi] = thr_final;
@@ -731,9 +834,9 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
                        const void* pmax, const int32_t* pairs, int P, float ratio,
                        RowBest* rows, int max_rows, uint32_t* cand, int32_t* cand_n, float* cand_thr,
                        int* ovf_count, int2* ovf_list, hipStream_t st) {
-  static const int abl = [] {
-    const char* e = getenv("SFMFEAT_MATCH_ABL");  // diagnostics only (tools/bench_match.py)
-    return e ? atoi(e) : 0;
+  static const int stage = [] {  // SFMFEAT_MATCH_STAGE=reg: register-staged sweep (A/B timing)
+    const char* e = getenv("SFMFEAT_MATCH_STAGE");
+    return (e && e[0] == 'r') ? 0 : 1;
   }();
   static const int rr8_max = [] {  // SFMFEAT_RERANK8_MAX: pair-count switch (A/B timing)
     const char* e = getenv("SFMFEAT_RERANK8_MAX");
@@ -742,32 +845,24 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
   const int qb = (max_rows + kQB - 1) / kQB;
   const dim3 grid((unsigned)(8 * ((P + 7) / 8) * qb));
   // ovf_count is zero here: set once at allocation, re-zeroed by k_match_compact
-#define SFM_SWEEP(A)                                                                                           \
-  hipLaunchKernelGGL(k_match_mfma<A>, grid, dim3(kNT), 0, st, count, capP, hi, lo, norm2, rnorm,                 \
-                     static_cast<const float2*>(pmax), pairs, P,                                                  \
-                     max_rows, cand, cand_n, cand_thr, ovf_count, ovf_list)
-  if (abl == 9)
-    SFM_SWEEP(9);
-  else if (abl == 10)
-    SFM_SWEEP(10);
-  else if (abl == 11)
-    SFM_SWEEP(11);
-  else if (abl == 12)
-    SFM_SWEEP(12);
-  else
+#define SFM_SWEEP(A)                                                                                  \
+  hipLaunchKernelGGL(k_match_mfma<A>, grid, dim3(kNT), 0, st, count, capP, hi, lo, norm2, rnorm,        \
+                     static_cast<const float2*>(pmax), pairs, P, max_rows, cand, cand_n, cand_thr, ovf_count, \
+                     ovf_list)
+  if (stage == 0)
     SFM_SWEEP(0);
+  else
+    SFM_SWEEP(1);
 #undef SFM_SWEEP
-  if (abl == 0 || abl == 6) {  // 6: no re-rank (timing)
-    if (abl == 0 && P <= rr8_max)
-      hipLaunchKernelGGL(k_match_rerank8, dim3((unsigned)(((int64_t)P * max_rows + 4 * kRrRows - 1) / (4 * kRrRows))),
-                         dim3(256), 0, st, desc, count, cap, pairs, P, ratio, max_rows, cand, cand_n, cand_thr, rows);
-    else if (abl == 0)
-      hipLaunchKernelGGL(k_match_rerank, dim3((unsigned)(((int64_t)P * max_rows + 3) / 4)), dim3(256), 0, st, desc,
-                         count, cap, pairs, P, ratio, max_rows, cand, cand_n, cand_thr, rows);
-    // the overflow list's length stays on the device: a fixed grid strides over it
-    hipLaunchKernelGGL(k_match_overflow, dim3(256), dim3(256), 0, st, desc, count, cap, pairs, ratio, rows,
-                       max_rows, ovf_count, ovf_list);
-  }
+  if (P <= rr8_max)
+    hipLaunchKernelGGL(k_match_rerank8, dim3((unsigned)(((int64_t)P * max_rows + 4 * kRrRows - 1) / (4 * kRrRows))),
+                       dim3(256), 0, st, desc, count, cap, pairs, P, ratio, max_rows, cand, cand_n, cand_thr, rows);
+  else
+    hipLaunchKernelGGL(k_match_rerank, dim3((unsigned)(((int64_t)P * max_rows + 3) / 4)), dim3(256), 0, st, desc,
+                       count, cap, pairs, P, ratio, max_rows, cand, cand_n, cand_thr, rows);
+  // the overflow list's length stays on the device: a fixed grid strides over it
+  hipLaunchKernelGGL(k_match_overflow, dim3(256), dim3(256), 0, st, desc, count, cap, pairs, ratio, rows, max_rows,
+                     ovf_count, ovf_list);
 }
 
 }  // namespace sfm
