@@ -280,6 +280,11 @@ int32_t sfm_debug_nms(int32_t device, const float* R, int32_t B, int32_t H, int3
  * (0 full, 1 no digit histogram, 2 window sums over the first tap row only). */
 float sfm_debug_time_harris(int32_t device, int32_t abl, int32_t B, int32_t H, int32_t W,
                             int32_t iters);
+/* As sfm_debug_time_harris; abl = 3 (full kernel + timestamps) also copies the last launch's
+   per-workgroup records into out[cap] (48 u64 per workgroup: start, end, CU id, tiles, then
+   the end of each tile; s_memrealtime ticks of 10 ns). */
+float sfm_debug_harris_stamps(int32_t device, int32_t abl, int32_t B, int32_t H, int32_t W,
+                              int32_t iters, uint64_t* out, int64_t cap);
 
 /* Keypoint selection of the context's last extraction (synchronises the device): planes
  * (image x level) that took the exact-median path, and planes in total.  The default

@@ -127,7 +127,19 @@ int32_t sfm_debug_nms(int32_t device, const float* R, int32_t B, int32_t H, int3
 // Mean time (ms) of one k_harris<7> launch over B x H x W synthetic planes for ablation
 // variant `abl` (0 full, 1 no histogram, 2 no window sums, 3 no Sobel/products).
 float sfm_debug_time_harris(int32_t device, int32_t abl, int32_t B, int32_t H, int32_t W, int32_t iters) {
+  return sfm_debug_harris_stamps(device, abl, B, H, W, iters, nullptr, 0);
+}
+
+// As sfm_debug_time_harris; abl = 3 also copies the last launch's per-workgroup timestamps
+// (48 u64 per workgroup, workgroup (x, plane) at (plane * grid_x + x) * 48) into `out`.
+float sfm_debug_harris_stamps(int32_t device, int32_t abl, int32_t B, int32_t H, int32_t W, int32_t iters,
+                              uint64_t* out, int64_t cap) {
   if (hipSetDevice(device) != hipSuccess) return -1.0f;
+  uint64_t* d_st = nullptr;
+  if (abl == 3) {
+    if (cap <= 0 || hipMalloc(&d_st, (size_t)cap * 8) != hipSuccess) return -1.0f;
+    (void)hipMemset(d_st, 0, (size_t)cap * 8);
+  }
   int64_t n = (int64_t)B * H * W;
   float *d_img = nullptr, *d_R = nullptr, *d_g = nullptr;
   uint32_t* d_hist = nullptr;
@@ -145,7 +157,11 @@ float sfm_debug_time_harris(int32_t device, int32_t abl, int32_t B, int32_t H, i
   (void)hipMemcpy(d_img, h.data(), n * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(d_g, g, 4 * 49, hipMemcpyHostToDevice);
   (void)hipMemset(d_hist, 0, (size_t)B * 4 * kMedBins1);
-  float ms = time_harris_ablation(abl, d_img, d_R, d_hist, B, H, W, d_g, 0.05f, iters);
+  float ms = time_harris_ablation(abl, d_img, d_R, d_hist, B, H, W, d_g, 0.05f, iters, d_st);
+  if (d_st) {
+    (void)hipMemcpy(out, d_st, (size_t)cap * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d_st);
+  }
   void* bufs[] = {d_img, d_R, d_g, d_hist};
   for (void* b : bufs) (void)hipFree(b);
   return ms;

@@ -58,7 +58,12 @@ __device__ __forceinline__ void pk_fma_bcast(f32x2& acc, f32x2 k, f32x2 v) {
 // registers one tile ahead.
 //
 // ABL (timing builds only): 0 = full kernel, 1 = no digit histogram, 2 = window sums over
-// the first tap row only.
+// the first tap row only, 3 = full kernel + per-workgroup timestamps into g_harris_stamps.
+// ABL = 3 diagnostics: per workgroup kStampSlots u64 = {start, end, cu id, tiles, end of
+// each tile ...} (s_memrealtime, 100 MHz)
+constexpr int kStampSlots = 48;
+__device__ uint64_t* g_harris_stamps;
+
 template <int KS, bool VEC, int ABL = 0>
 __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float* __restrict__ gk, float alpha) {
   // this workgroup's level (one launch may hold several pyramid levels: the small levels'
@@ -101,6 +106,15 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
 
   const int tid = threadIdx.x;
   const int b = blockIdx.y;
+  uint64_t* stamp = nullptr;
+  int nst = 0;
+  if constexpr (ABL == 3) {
+    stamp = g_harris_stamps + ((int64_t)b * gridDim.x + blockIdx.x) * kStampSlots;
+    if (tid == 0) {
+      stamp[0] = wall_clock64();
+      stamp[2] = (uint64_t)__smid();
+    }
+  }
   const float* img = lvl + (int64_t)b * H * W;
   float* Rp = Rout + (int64_t)b * H * W;
   for (int i = tid; i < kMedBins1; i += 256) s_hist[i] = 0u;
@@ -354,7 +368,17 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
         }
       }
     }
+    if constexpr (ABL == 3) {
+      if (tid == 0 && nst < kStampSlots - 4) stamp[4 + nst] = wall_clock64();
+      ++nst;
+    }
   }  // tile loop
+  if constexpr (ABL == 3) {
+    if (tid == 0) {
+      stamp[1] = wall_clock64();
+      stamp[3] = (uint64_t)nst;
+    }
+  }
   __syncthreads();
   uint32_t* hg = hist_g + (int64_t)b * kMedBins1;
   for (int i = tid; i < kMedBins1; i += 256) {
@@ -456,7 +480,8 @@ void launch_harris(const float* lvl, float* R, uint32_t* hist, int B, int H, int
 
 // Ablation timing (diagnostics): KS = 7 only, returns the mean launch time in ms.
 float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
-                           const float* gk, float alpha, int iters) {
+                           const float* gk, float alpha, int iters, uint64_t* stamps) {
+  if (abl == 3) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_harris_stamps), &stamps, sizeof(stamps));
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
@@ -472,6 +497,7 @@ float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, 
     switch (abl) {
       case 1: launch_ks<7, 1>(g, B, gk, alpha, 0); break;
       case 2: launch_ks<7, 2>(g, B, gk, alpha, 0); break;
+      case 3: launch_ks<7, 3>(g, B, gk, alpha, 0); break;
       default: launch_ks<7, 0>(g, B, gk, alpha, 0); break;
     }
   };

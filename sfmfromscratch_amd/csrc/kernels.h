@@ -114,6 +114,38 @@ SFM_DEV void select_scan_plane(const uint32_t* hist, MedianState* st, unsigned l
   }
 }
 
+// Resolve one rank within bucket `bk` (the key's top 11 bits) from a collected list of keys
+// (exact median, digits 2 and 3; every thread of the block calls it).
+SFM_DEV uint32_t select_in_list(const uint32_t* lp, int64_t m, uint32_t bk, uint32_t rank,
+                                uint32_t* s_h, uint32_t* s_scan, uint32_t* s_out) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  // digit 2: bits [20:10]
+  for (int i = tid; i < kHistBins; i += nt) s_h[i] = 0u;
+  __syncthreads();
+  for (int64_t i = tid; i < m; i += nt) {
+    uint32_t k = lp[i];
+    if ((k >> 21) == bk) atomicAdd(&s_h[(k >> 10) & 0x7ffu], 1u);
+  }
+  __syncthreads();
+  find_bin(s_h, kHistBins, rank, s_scan, s_out);
+  uint32_t d2 = s_out[0];
+  rank -= s_out[1];
+  uint32_t pre = (bk << 11) | d2;  // top 22 bits
+  __syncthreads();
+  // digit 3: bits [9:0] (histogram padded to 4096 bins for find_bin)
+  for (int i = tid; i < kHistBins; i += nt) s_h[i] = 0u;
+  __syncthreads();
+  for (int64_t i = tid; i < m; i += nt) {
+    uint32_t k = lp[i];
+    if ((k >> 10) == pre) atomicAdd(&s_h[k & 0x3ffu], 1u);
+  }
+  __syncthreads();
+  find_bin(s_h, kHistBins, rank, s_scan, s_out);
+  uint32_t d3 = s_out[0];
+  __syncthreads();
+  return (pre << 10) | d3;
+}
+
 // Arguments of the select scan fused into the Harris launch (state == nullptr: not fused).
 struct SelectScan {
   MedianState* state;                  // [B]
@@ -180,7 +212,7 @@ void launch_harris_levels(const HarrisLevels& g, int B, const float* d_gauss, in
                           hipStream_t st);
 
 float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
-                           const float* gk, float alpha, int iters);
+                           const float* gk, float alpha, int iters, uint64_t* stamps = nullptr);
 
 // median.hip.  launch_select_scan: median buckets + certified threshold per plane
 // (vmin = pixels required at or above the threshold).  launch_median_exact: the exact
@@ -198,15 +230,17 @@ void launch_nms(const float* R, const MedianState* state, uint64_t* cand,
                 unsigned long long* cand_count, int B, int H, int W, int ksize, int mode, hipStream_t st,
                 int force_tile = 0);
 
-// select.hip: top-k by (conf desc, index asc) + edge filter (NaiveSIFT.py:99-120).
+// select.hip: keypoint selection of one level, one workgroup per plane: top-k by (conf
+// desc, index asc) of the certified NMS candidates + edge filter (NaiveSIFT.py:99-120);
+// planes that do not certify (or are flagged fallback already) run the exact path in the
+// same workgroup: exact median into state.median (medlist: n u32 per plane), the full NMS
+// predicate into cand (n u64 per plane), then the same top-k.  scratch: n u64 per plane.
 void init_topk_attributes();
 void init_describe_attributes(size_t max_lds);
 size_t describe_lds_bytes(int fw, int rotate);
-// mode 0: certified planes (a plane with fewer than k candidates is flagged fallback and
-// left unwritten); mode 1: fallback planes only.
-void launch_topk(const uint64_t* cand, const unsigned long long* cand_count, uint64_t* scratch,
-                 KpList kp, int kcap, int k, int B, int H, int W, int half_window,
-                 MedianState* state, int mode, hipStream_t st);
+void launch_select(const float* R, uint64_t* cand, const unsigned long long* cand_count, uint32_t* medlist,
+                   uint64_t* scratch, KpList kp, int kcap, int k, int B, int H, int W, int ksize, int half_window,
+                   MedianState* state, hipStream_t st);
 
 // describe_q.hip: four keypoints per wavefront for window widths 2..22 (false: not handled)
 // out_count (the last level's launch): also write each slot's keypoint count

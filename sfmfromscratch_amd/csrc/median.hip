@@ -66,37 +66,6 @@ __global__ void __launch_bounds__(256) k_med_collect(const float* __restrict__ R
   }
 }
 
-// Resolve one rank within bucket `bk` (the key's top 11 bits) from the collected list.
-SFM_DEV uint32_t select_in_list(const uint32_t* lp, int64_t m, uint32_t bk, uint32_t rank,
-                                uint32_t* s_h, uint32_t* s_scan, uint32_t* s_out) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-  // digit 2: bits [20:10]
-  for (int i = tid; i < kHistBins; i += nt) s_h[i] = 0u;
-  __syncthreads();
-  for (int64_t i = tid; i < m; i += nt) {
-    uint32_t k = lp[i];
-    if ((k >> 21) == bk) atomicAdd(&s_h[(k >> 10) & 0x7ffu], 1u);
-  }
-  __syncthreads();
-  find_bin(s_h, kHistBins, rank, s_scan, s_out);
-  uint32_t d2 = s_out[0];
-  rank -= s_out[1];
-  uint32_t pre = (bk << 11) | d2;  // top 22 bits
-  __syncthreads();
-  // digit 3: bits [9:0] (histogram padded to 4096 bins for find_bin)
-  for (int i = tid; i < kHistBins; i += nt) s_h[i] = 0u;
-  __syncthreads();
-  for (int64_t i = tid; i < m; i += nt) {
-    uint32_t k = lp[i];
-    if ((k >> 10) == pre) atomicAdd(&s_h[k & 0x3ffu], 1u);
-  }
-  __syncthreads();
-  find_bin(s_h, kHistBins, rank, s_scan, s_out);
-  uint32_t d3 = s_out[0];
-  __syncthreads();
-  return (pre << 10) | d3;
-}
-
 __global__ void __launch_bounds__(1024) k_med_final(MedianState* __restrict__ st,
                                                     const uint32_t* __restrict__ list,
                                                     const unsigned long long* __restrict__ list_count,

@@ -1,15 +1,21 @@
-// select.hip — top-k + edge filter per plane (NaiveSIFT.py:99-120):
-//   sort_filter = argsort(conf)[::-1][:k]   -> k smallest 64-bit candidate keys
-//   edge filter h <= y < H-h, h <= x < W-h  (h = feature_width // 2), applied AFTER top-k
-//   re-sort descending                      -> keys stay in ascending key order
-// One 1024-thread workgroup per plane.  Up to kTopkDirect candidates are sorted directly
-// in LDS; beyond that a block radix select on the confidence half of the key finds the
-// k-th key (ties on confidence resolved by raster index, exactly), and only the
-// selected k keys are sorted.
+// select.hip — keypoint selection per plane (NaiveSIFT.py:90-120), one 1024-thread
+// workgroup per plane, one launch per pyramid level:
+//   certified select : the k smallest 64-bit candidate keys of the certified NMS pass
+//                      (sort_filter = argsort(conf)[::-1][:k]); final when the k-th key
+//                      reaches tcert (kernels.h, MedianState);
+//   exact path       : planes that do not certify (and levels too small to, and forced
+//                      exact mode) continue in the same workgroup — np.median by radix
+//                      select (:91), the full NMS predicate with that median (:77-97), then
+//                      the same top-k over those candidates;
+//   edge filter      : h <= y < H-h, h <= x < W-h (h = feature_width // 2), applied AFTER
+//                      top-k; keys stay in ascending key order (confidence descending).
+// Up to kTopkDirect candidates are sorted directly in LDS; beyond that a block radix select
+// on the confidence half of the key finds the k-th key (ties on confidence resolved by
+// raster index, exactly), and only the selected k keys are sorted.
 //
-// mode 0 (certified select, kernels.h MedianState): a plane is final when it has at least
-// k candidates and the k-th key reaches tcert; otherwise it is flagged `fallback` and left
-// to mode 1, which runs after the exact median + NMS on the flagged planes only.
+// The exact path used to be four launches per level (median collect, median final, NMS,
+// top-k) that exited at once on certified planes; a plane's exact path now runs in the
+// workgroup that found it uncertified, so a certified level costs one launch in all.
 #include "kernels.h"
 
 namespace sfm {
@@ -54,111 +60,90 @@ SFM_DEV uint32_t radix_select_u32(const uint64_t* arr, int64_t m, bool use_lo, u
   return prefix;
 }
 
-__global__ void __launch_bounds__(1024) k_topk(const uint64_t* __restrict__ cand,
-                                               const unsigned long long* __restrict__ cand_count,
-                                               uint64_t* __restrict__ scratch, KpList kp, int kcap,
-                                               int k, int H, int W, int hw,
-                                               MedianState* __restrict__ state, int mode) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
-  uint64_t* s_sel = reinterpret_cast<uint64_t*>(s_raw);               // kTopkLdsCap
-  uint64_t* s_tie = s_sel + kTopkLdsCap;                               // kTieLdsCap
-  uint32_t* s_h = reinterpret_cast<uint32_t*>(s_tie + kTieLdsCap);     // kHistBins
-  uint32_t* s_scan = s_h + kHistBins;                                  // 1024
-  __shared__ uint32_t s_out[2];
-  __shared__ uint32_t s_cnt[2];
+struct SelectLds {
+  uint64_t* sel;   // kTopkLdsCap
+  uint64_t* tie;   // kTieLdsCap
+  uint32_t* h;     // kHistBins
+  uint32_t* scan;  // 1024
+  uint32_t* out;   // 2
+  uint32_t* cnt;   // 2
+};
 
+// The kk (>= 1) smallest of the C keys cp[0..C) into L.sel[0..kk), ascending (tp: per-plane
+// scratch for tie lists that overflow LDS).
+SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, const SelectLds& L) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  const int b = blockIdx.x;
-  const int64_t n = (int64_t)H * W;
-  const uint64_t* cp = cand + (int64_t)b * n;
-  const int64_t C = (int64_t)cand_count[(int64_t)b * kCounterStride];
-  if (mode == 0) {
-    if (state[b].fallback) return;
-    if (C < (int64_t)k) {  // cannot certify: the exact path decides this plane
-      if (tid == 0) state[b].fallback = 1u;
-      return;
-    }
-  } else if (!state[b].fallback) {
-    return;
-  }
-  const int kk = (int)((int64_t)k < C ? (int64_t)k : C);
-  if (kk <= 0) {
-    if (tid == 0) kp.count[b] = 0;
-    return;
-  }
-  int nsel;
   if (C <= kTopkDirect) {
     const int P = next_pow2((int)C);
-    for (int i = tid; i < P; i += nt) s_sel[i] = (i < C) ? cp[i] : ~0ull;
+    for (int i = tid; i < P; i += nt) L.sel[i] = (i < C) ? cp[i] : ~0ull;
     __syncthreads();
-    bitonic_sort_u64(s_sel, P);
-    nsel = kk;
-  } else {
-    uint32_t rank = (uint32_t)(kk - 1);
-    const uint32_t T = radix_select_u32(cp, C, false, 0u, &rank, s_h, s_scan, s_out);
-    if (tid == 0) { s_cnt[0] = 0u; s_cnt[1] = 0u; }
-    __syncthreads();
-    uint64_t* tp = scratch + (int64_t)b * n;
-    for (int64_t i = tid; i < C; i += nt) {
-      uint64_t key = cp[i];
-      uint32_t hi = (uint32_t)(key >> 32);
-      if (hi < T) {
-        s_sel[atomicAdd(&s_cnt[0], 1u)] = key;
-      } else if (hi == T) {
-        uint32_t t = atomicAdd(&s_cnt[1], 1u);
-        if (t < kTieLdsCap) s_tie[t] = key;
-        tp[t] = key;
-      }
-    }
-    __syncthreads();
-    const uint32_t nless = s_cnt[0];
-    const uint32_t ntie = s_cnt[1];
-    const uint32_t need = rank + 1;  // ties taken, by ascending raster index
-    if (ntie <= (uint32_t)kTieLdsCap) {
-      const int P = next_pow2((int)ntie);
-      for (int i = tid; i < P; i += nt)
-        if (i >= (int)ntie) s_tie[i] = ~0ull;
-      __syncthreads();
-      bitonic_sort_u64(s_tie, P);
-      for (uint32_t i = tid; i < need; i += nt) s_sel[nless + i] = s_tie[i];
-    } else {
-      uint32_t r2 = rank;
-      const uint32_t Tlo = radix_select_u32(tp, ntie, true, T, &r2, s_h, s_scan, s_out);
-      for (int64_t i = tid; i < ntie; i += nt) {
-        uint64_t key = tp[i];
-        if ((uint32_t)key <= Tlo) s_sel[atomicAdd(&s_cnt[0], 1u)] = key;
-      }
-    }
-    __syncthreads();
-    nsel = kk;
-    const int P = next_pow2(nsel);
-    for (int i = tid; i < P; i += nt)
-      if (i >= nsel) s_sel[i] = ~0ull;
-    __syncthreads();
-    bitonic_sort_u64(s_sel, P);
-  }
-  __syncthreads();
-  if (mode == 0 && kk > 0 && ~(uint32_t)(s_sel[kk - 1] >> 32) < state[b].tcert) {
-    if (tid == 0) state[b].fallback = 1u;  // k-th candidate not above the median's bucket
+    bitonic_sort_u64(L.sel, P);
     return;
   }
-  // edge filter with order-preserving compaction
+  uint32_t rank = (uint32_t)(kk - 1);
+  const uint32_t T = radix_select_u32(cp, C, false, 0u, &rank, L.h, L.scan, L.out);
+  if (tid == 0) {
+    L.cnt[0] = 0u;
+    L.cnt[1] = 0u;
+  }
+  __syncthreads();
+  for (int64_t i = tid; i < C; i += nt) {
+    const uint64_t key = cp[i];
+    const uint32_t hi = (uint32_t)(key >> 32);
+    if (hi < T) {
+      L.sel[atomicAdd(&L.cnt[0], 1u)] = key;
+    } else if (hi == T) {
+      const uint32_t t = atomicAdd(&L.cnt[1], 1u);
+      if (t < kTieLdsCap) L.tie[t] = key;
+      tp[t] = key;
+    }
+  }
+  __syncthreads();
+  const uint32_t nless = L.cnt[0];
+  const uint32_t ntie = L.cnt[1];
+  const uint32_t need = rank + 1;  // ties taken, by ascending raster index
+  if (ntie <= (uint32_t)kTieLdsCap) {
+    const int P = next_pow2((int)ntie);
+    for (int i = tid; i < P; i += nt)
+      if (i >= (int)ntie) L.tie[i] = ~0ull;
+    __syncthreads();
+    bitonic_sort_u64(L.tie, P);
+    for (uint32_t i = tid; i < need; i += nt) L.sel[nless + i] = L.tie[i];
+  } else {
+    uint32_t r2 = rank;
+    const uint32_t Tlo = radix_select_u32(tp, ntie, true, T, &r2, L.h, L.scan, L.out);
+    for (int64_t i = tid; i < ntie; i += nt) {
+      const uint64_t key = tp[i];
+      if ((uint32_t)key <= Tlo) L.sel[atomicAdd(&L.cnt[0], 1u)] = key;
+    }
+  }
+  __syncthreads();
+  const int P = next_pow2(kk);
+  for (int i = tid; i < P; i += nt)
+    if (i >= kk) L.sel[i] = ~0ull;
+  __syncthreads();
+  bitonic_sort_u64(L.sel, P);
+}
+
+// Edge filter with order-preserving compaction of L.sel[0..nsel) into the plane's list.
+SFM_DEV void emit_keypoints(const SelectLds& L, int nsel, KpList kp, int b, int kcap, int H, int W, int hw) {
+  const int tid = threadIdx.x, nt = blockDim.x;
   const int per = (nsel + nt - 1) / nt;
   const int beg = tid * per;
   uint32_t local = 0;
   for (int i = beg; i < beg + per && i < nsel; ++i) {
-    uint32_t idx = (uint32_t)s_sel[i];
-    int y = (int)(idx / (uint32_t)W), x = (int)(idx % (uint32_t)W);
+    const uint32_t idx = (uint32_t)L.sel[i];
+    const int y = (int)(idx / (uint32_t)W), x = (int)(idx % (uint32_t)W);
     local += (y >= hw && y < H - hw && x >= hw && x < W - hw) ? 1u : 0u;
   }
   uint32_t total;
-  uint32_t pos = block_exclusive_scan(local, s_scan, &total);
+  uint32_t pos = block_exclusive_scan(local, L.scan, &total);
   for (int i = beg; i < beg + per && i < nsel; ++i) {
-    uint64_t key = s_sel[i];
-    uint32_t idx = (uint32_t)key;
-    int y = (int)(idx / (uint32_t)W), x = (int)(idx % (uint32_t)W);
+    const uint64_t key = L.sel[i];
+    const uint32_t idx = (uint32_t)key;
+    const int y = (int)(idx / (uint32_t)W), x = (int)(idx % (uint32_t)W);
     if (y >= hw && y < H - hw && x >= hw && x < W - hw) {
-      int64_t o = (int64_t)b * kcap + pos;
+      const int64_t o = (int64_t)b * kcap + pos;
       kp.x[o] = x;
       kp.y[o] = y;
       kp.conf[o] = fkey_inv(~(uint32_t)(key >> 32));
@@ -168,19 +153,151 @@ __global__ void __launch_bounds__(1024) k_topk(const uint64_t* __restrict__ cand
   if (tid == 0) kp.count[b] = (int32_t)total;
 }
 
+// Wave-aggregated append to an LDS counter: the lane's slot, or -1 without pred.
+SFM_DEV int lds_wave_append(uint32_t* counter, bool pred) {
+  const uint64_t mask = __ballot(pred);
+  if (mask == 0) return -1;
+  const int lane = __lane_id();
+  const int leader = __ffsll((unsigned long long)mask) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+  base = __shfl(base, leader);
+  const uint64_t lower = mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane)));
+  return pred ? (int)(base + (uint32_t)__popcll(lower)) : -1;
+}
+
+// np.median of the plane (NaiveSIFT.py:91): the keys of the two digit-1 buckets holding the
+// middle ranks (from the Harris histogram's select scan) are collected into `list`, then
+// digits 2 and 3 resolved by select_in_list.  Even n: float32 (v[n/2-1] + v[n/2]) / 2.
+SFM_DEV float exact_median(const float* Rp, int64_t n, const MedianState& s, uint32_t* list, const SelectLds& L) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (tid == 0) L.cnt[0] = 0u;
+  __syncthreads();
+  const uint32_t b1 = s.bucket[0], b2 = s.bucket[1];
+  for (int64_t base = 0; base < n; base += nt) {
+    const int64_t i = base + tid;
+    uint32_t key = 0;
+    bool in = false;
+    if (i < n) {
+      key = fkey(Rp[i]);
+      const uint32_t d = key >> (32 - kMedBits1);
+      in = d == b1 || d == b2;
+    }
+    const int slot = lds_wave_append(&L.cnt[0], in);
+    if (in) list[slot] = key;
+  }
+  __syncthreads();
+  const int64_t m = (int64_t)L.cnt[0];
+  __syncthreads();
+  const uint32_t key1 = select_in_list(list, m, b1, s.rank[0], L.h, L.scan, L.out);
+  const float v1 = fkey_inv(key1);
+  if (s.odd) return v1;
+  const uint32_t key2 = select_in_list(list, m, b2, s.rank[1], L.h, L.scan, L.out);
+  const float v2 = fkey_inv(key2);
+  const float sum = v1 + v2;
+  return sum / 2.0f;
+}
+
+// The reference's NMS predicate with the exact median (nms.hip, mode 1): candidate <=>
+// (R >= med && no cell of the clipped (2kh+1)^2 window is larger) || (R < med && R == 0).
+// One wavefront per row; candidates appended to cp (any order: top-k orders them).
+SFM_DEV int64_t exact_nms(const float* Rp, int H, int W, int kh, float med, uint64_t* cp, const SelectLds& L) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+  if (tid == 0) L.cnt[1] = 0u;
+  __syncthreads();
+  for (int y = wid; y < H; y += nw) {
+    const int y0 = max(y - kh, 0), y1 = min(y + kh, H - 1);
+    for (int xb = 0; xb < W; xb += 64) {
+      const int x = xb + lane;
+      bool pred = false;
+      float v = 0.0f;
+      if (x < W) {
+        v = Rp[(int64_t)y * W + x];
+        if (v < med) {
+          pred = v == 0.0f;  // R_maxpool[R < median] = 0 (:92)
+        } else {
+          const int x0 = max(x - kh, 0), x1 = min(x + kh, W - 1);
+          bool ismax = true;
+          for (int yy = y0; yy <= y1; ++yy) {
+            const float* row = Rp + (int64_t)yy * W;
+            for (int xx = x0; xx <= x1; ++xx) ismax &= !(row[xx] > v);
+          }
+          pred = ismax;
+        }
+      }
+      const int slot = lds_wave_append(&L.cnt[1], pred);
+      if (pred) cp[slot] = ((uint64_t)(~fkey(v)) << 32) | (uint32_t)(y * W + x);
+    }
+  }
+  __syncthreads();
+  const int64_t C = (int64_t)L.cnt[1];
+  __syncthreads();
+  return C;
+}
+
+__global__ void __launch_bounds__(1024) k_select(const float* __restrict__ R, uint64_t* __restrict__ cand,
+                                                 const unsigned long long* __restrict__ cand_count,
+                                                 uint32_t* __restrict__ medlist, uint64_t* __restrict__ scratch,
+                                                 KpList kp, int kcap, int k, int H, int W, int kh, int hw,
+                                                 MedianState* __restrict__ state) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
+  __shared__ uint32_t s_out[2];
+  __shared__ uint32_t s_cnt[2];
+  SelectLds L;
+  L.sel = reinterpret_cast<uint64_t*>(s_raw);
+  L.tie = L.sel + kTopkLdsCap;
+  L.h = reinterpret_cast<uint32_t*>(L.tie + kTieLdsCap);
+  L.scan = L.h + kHistBins;
+  L.out = s_out;
+  L.cnt = s_cnt;
+
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x;
+  const int64_t n = (int64_t)H * W;
+  uint64_t* cp = cand + (int64_t)b * n;
+  uint64_t* tp = scratch + (int64_t)b * n;
+  const MedianState s = state[b];
+  if (k <= 0) {
+    if (tid == 0) kp.count[b] = 0;
+    return;
+  }
+  if (!s.fallback) {
+    const int64_t C = (int64_t)cand_count[(int64_t)b * kCounterStride];
+    if (C >= (int64_t)k) {
+      topk_sorted(cp, C, k, tp, L);
+      if (~(uint32_t)(L.sel[k - 1] >> 32) >= s.tcert) {  // k-th candidate above the median's bucket
+        emit_keypoints(L, k, kp, b, kcap, H, W, hw);
+        return;
+      }
+    }
+    // cannot certify (fewer than k candidates, or the k-th not above the median's bucket)
+    if (tid == 0) state[b].fallback = 1u;
+  }
+  const float med = exact_median(R + (int64_t)b * n, n, s, medlist + (int64_t)b * n, L);
+  if (tid == 0) state[b].median = med;
+  const int64_t C = exact_nms(R + (int64_t)b * n, H, W, kh, med, cp, L);
+  const int kk = (int)((int64_t)k < C ? (int64_t)k : C);
+  if (kk <= 0) {
+    if (tid == 0) kp.count[b] = 0;
+    return;
+  }
+  topk_sorted(cp, C, kk, tp, L);
+  emit_keypoints(L, kk, kp, b, kcap, H, W, hw);
+}
+
 size_t topk_lds_bytes() {
   return (size_t)kTopkLdsCap * 8 + (size_t)kTieLdsCap * 8 + (size_t)kHistBins * 4 + 1024 * 4;
 }
 
-void launch_topk(const uint64_t* cand, const unsigned long long* cand_count, uint64_t* scratch,
-                 KpList kp, int kcap, int k, int B, int H, int W, int half_window,
-                 MedianState* state, int mode, hipStream_t st) {
-  hipLaunchKernelGGL(k_topk, dim3(B), dim3(1024), topk_lds_bytes(), st, cand, cand_count, scratch, kp,
-                     kcap, k, H, W, half_window, state, mode);
+void launch_select(const float* R, uint64_t* cand, const unsigned long long* cand_count, uint32_t* medlist,
+                   uint64_t* scratch, KpList kp, int kcap, int k, int B, int H, int W, int ksize, int half_window,
+                   MedianState* state, hipStream_t st) {
+  hipLaunchKernelGGL(k_select, dim3(B), dim3(1024), topk_lds_bytes(), st, R, cand, cand_count, medlist, scratch, kp,
+                     kcap, k, H, W, ksize / 2, half_window, state);
 }
 
 void init_topk_attributes() {
-  (void)hipFuncSetAttribute((const void*)k_topk, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)topk_lds_bytes());
 }
 

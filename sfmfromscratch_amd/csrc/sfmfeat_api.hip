@@ -331,28 +331,14 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     // path (a size-only decision: no host synchronisation)
     e.exact = c->exact_select || (int64_t)h * w < (int64_t)64 * c->kcap;
   }
-  auto select_level = [&](int l, hipStream_t s) {  // top-k + exact fallback of level l
+  auto select_level = [&](int l, hipStream_t s) {  // top-k, exact path in the same launch
     const LevelBufs& e = lb[l];
-    const int h = lv[l].h, w = lv[l].w;
-    if (!e.exact) {
-      StageScope sc(c, SFM_PROF_TOPK, s);
-      // the scratch region of this level's stream (the aux stream's levels and the caller
-      // stream's levels select concurrently)
-      launch_topk(e.cand, candcnt + e.co, as<uint64_t>(c->d_scratch) + (l < L_aux ? 0 : (int64_t)B * H * W), e.kp,
-                  std::max(c->kcap, 1), c->kcap, B, h, w, lv[l].fw / 2, e.med, 0, s);
-    }
-    {
-      StageScope sc(c, SFM_PROF_MEDIAN, s);
-      launch_median_exact(e.R, e.med, as<uint32_t>(c->d_medlist) + (l < L_aux ? 0 : (int64_t)B * H * W), medcnt + e.co,
-                          B, h, w, s);
-    }
-    {
-      StageScope sc(c, SFM_PROF_NMS, s);
-      launch_nms(e.R, e.med, e.cand, candcnt2 + e.co, B, h, w, c->p.ksize, 1, s);
-    }
     StageScope sc(c, SFM_PROF_TOPK, s);
-    launch_topk(e.cand, candcnt2 + e.co, as<uint64_t>(c->d_scratch) + (l < L_aux ? 0 : (int64_t)B * H * W), e.kp,
-                std::max(c->kcap, 1), c->kcap, B, h, w, lv[l].fw / 2, e.med, 1, s);
+    // the scratch regions of this level's stream (the aux stream's levels and the caller
+    // stream's levels select concurrently)
+    const int64_t so = l < L_aux ? 0 : (int64_t)B * H * W;
+    launch_select(e.R, e.cand, candcnt + e.co, as<uint32_t>(c->d_medlist) + so, as<uint64_t>(c->d_scratch) + so, e.kp,
+                  std::max(c->kcap, 1), c->kcap, B, lv[l].h, lv[l].w, c->p.ksize, lv[l].fw / 2, e.med, s);
   };
   bool counted = false;  // the last level's describe launch wrote the slot counts
   auto describe_level = [&](int l, hipStream_t s) {
