@@ -2,19 +2,21 @@
 //
 // The reference's distances (NNRatioFeatureMatcher.py:31-34) are float32 pairwise sums;
 // its result only depends on, per query row, the two smallest distances and the argmin.
-// Those are found EXACTLY in three steps inside one workgroup of 128 query rows:
-//   1. approximate d^2 = |a|^2 + |b|^2 - 2 a.b for every target with fp16 split operands
-//      (a = hi + lo * 2^-11, three f16 MFMA products hi.hi + (hi.lo + lo.hi), f32
-//      accumulation, operands pre-scaled by 2^8 to keep them out of the f16 subnormal
-//      range), tracking each row's second-smallest approximate value D2~ (sweep 1);
-//   2. a second sweep collects every target with d~ <= D2~ + 2 E_i, where E_i bounds
-//      |d~ - d_ref| rigorously (fp16 representation, dropped lo.lo term, f32 accumulation
-//      error <= K u sum|ab|, f32 rounding of d~ and of the reference's own pairwise sum):
-//      any target outside that window is strictly farther than the second nearest;
-//   3. recompute the window with the reference's exact float32 pairwise order (8
-//      accumulators) and take (distance, index) minima -> ratio test.
-// Rows whose window overflows the per-row LDS list (runs of near-identical target
-// descriptors) are recomputed exactly over all targets by k_match_overflow.
+// Those are found EXACTLY by:
+//   1. k_match_mfma: ONE sweep per (pair, 256 query rows) over the target table computing
+//      approximate d~ = |a|^2 + |b|^2 - 2 a.b with fp16 split operands (a = hi + lo 2^-11,
+//      three f16 MFMA products hi.hi + (hi.lo + lo.hi), f32 accumulation, operands
+//      pre-scaled by 2^8 out of the f16 subnormal range).  Each row keeps a running top-2
+//      of d~ and appends to its window list every target with d~ <= b2~(so far) + 2 E_i,
+//      where E_i bounds |d~ - d_ref| rigorously (fp16 representation, dropped lo.lo term,
+//      f32 accumulation error, f32 rounding of d~ and of the reference's own pairwise
+//      sum); any target outside the final window is strictly farther than the second
+//      nearest (argument above k_match_mfma);
+//   2. k_match_rerank: the list entries within the row's final threshold recomputed with the
+//      reference's exact float32 pairwise order (8 accumulators), (distance, index) top-2,
+//      ratio test;
+//   3. k_match_overflow: rows whose list overflowed (runs of near-identical target
+//      descriptors) recomputed exactly over every target.
 #include <stdlib.h>
 
 #include <type_traits>
@@ -188,8 +190,9 @@ __device__ __forceinline__ void glds_x1(const void* gsrc, uint32_t lds_dst) {
 //     barrier (counted vmcnt, raw s_barrier); the appends' stores come before it in issue
 //     order, so the count stays static.
 //   0: register staging (global -> VGPRs -> ds_write into padded rows), two buffers (A/B).
-// Per element the epilogue forms d~, updates the row's running top-2 (two v_med3) and admits
-// the target when d~ <= thr, thr = b2~(so far) + 2E: this lane's own b2~ after the sub-tile,
+// Per element the epilogue forms d~; per sub-tile a tournament gives the lane's two smallest,
+// merged into the row's running top-2, and a target is admitted when d~ <= thr,
+// thr = b2~(so far) + 2E: this lane's own b2~ after the sub-tile,
 // capped by the wave-merged b2~ of the previous stage.  b2~ only decreases, so every running
 // thr >= the final one and the admitted set contains the row's final window (argument
 // below).  thr uses the row's b2~ over both half-waves (merged after every sub-tile).
@@ -375,8 +378,7 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
                           // padding targets, d~ = +inf, are never admitted)
   // d~ = na + nb - 2 a.b with a.b = (ahh + ax 2^-11) 2^-16: two fmas by exact powers of two
   // (each rounding is covered by E's 4e-6 (na + nb) term); padding targets
-  // have norm2 = +inf: d~ = +inf.  Running top-2 (b2 = med3(b1, b2, d), b1 = min), then
-  // bit rr of mm for d~ <= min(b2~ + 2E, thr_w)
+  // have norm2 = +inf: d~ = +inf.  Bit rr of mm for d~ <= min(b2~ + 2E, thr_w).
   // The sub-tile's two smallest d~ by a tournament (pairs (min, max), then merges
   // m = min(ma, mb), s = min3(max(ma, mb), sa, sb)): the same multiset top-2 as an element-by-
   // element update, at a dependency depth of 9 instead of 32; merged into the running

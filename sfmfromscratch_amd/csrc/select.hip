@@ -60,6 +60,37 @@ SFM_DEV uint32_t radix_select_u32(const uint64_t* arr, int64_t m, bool use_lo, u
   return prefix;
 }
 
+// As radix_select_u32 (use_lo = false) over keys held in registers: thread t holds keys
+// t + 1024 j (j < R; absent keys are ~0 and never counted: their rank lies above every
+// real key's).  No global re-reads between the digit passes.
+template <int R>
+SFM_DEV uint32_t radix_select_regs(const uint64_t (&kr)[R], int64_t m, uint32_t* rank_io, uint32_t* s_h,
+                                   uint32_t* s_scan, uint32_t* s_out) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  uint32_t prefix = 0, mask = 0, rank = *rank_io;
+  const int shifts[3] = {20, 8, 0};
+  const uint32_t dmasks[3] = {0xfffu, 0xfffu, 0xffu};
+  for (int d = 0; d < 3; ++d) {
+    for (int i = tid; i < kHistBins; i += nt) s_h[i] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const uint32_t v = (uint32_t)(kr[j] >> 32);
+      if ((int64_t)tid + (int64_t)nt * j < m && (v & mask) == prefix) atomicAdd(&s_h[(v >> shifts[d]) & dmasks[d]], 1u);
+    }
+    __syncthreads();
+    find_bin(s_h, kHistBins, rank, s_scan, s_out);
+    prefix |= s_out[0] << shifts[d];
+    mask |= dmasks[d] << shifts[d];
+    rank -= s_out[1];
+    __syncthreads();
+  }
+  *rank_io = rank;
+  return prefix;
+}
+
+constexpr int kRegKeys = 8;  // keys per thread held in registers by the top-k (C <= 8192)
+
 struct SelectLds {
   uint64_t* sel;   // kTopkLdsCap
   uint64_t* tie;   // kTieLdsCap
@@ -81,14 +112,8 @@ SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, co
     return;
   }
   uint32_t rank = (uint32_t)(kk - 1);
-  const uint32_t T = radix_select_u32(cp, C, false, 0u, &rank, L.h, L.scan, L.out);
-  if (tid == 0) {
-    L.cnt[0] = 0u;
-    L.cnt[1] = 0u;
-  }
-  __syncthreads();
-  for (int64_t i = tid; i < C; i += nt) {
-    const uint64_t key = cp[i];
+  uint32_t T;  // confidence half of the k-th key
+  auto part = [&](uint64_t key) {  // keys below the k-th's confidence; its ties
     const uint32_t hi = (uint32_t)(key >> 32);
     if (hi < T) {
       L.sel[atomicAdd(&L.cnt[0], 1u)] = key;
@@ -97,6 +122,32 @@ SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, co
       if (t < kTieLdsCap) L.tie[t] = key;
       tp[t] = key;
     }
+  };
+  if (C <= (int64_t)kRegKeys * nt) {
+    // every key read once into registers (all loads in flight together)
+    uint64_t kr[kRegKeys];
+#pragma unroll
+    for (int j = 0; j < kRegKeys; ++j) {
+      const int64_t i = tid + (int64_t)nt * j;
+      kr[j] = i < C ? cp[i] : ~0ull;
+    }
+    T = radix_select_regs(kr, C, &rank, L.h, L.scan, L.out);
+    if (tid == 0) {
+      L.cnt[0] = 0u;
+      L.cnt[1] = 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kRegKeys; ++j)
+      if (tid + (int64_t)nt * j < C) part(kr[j]);
+  } else {
+    T = radix_select_u32(cp, C, false, 0u, &rank, L.h, L.scan, L.out);
+    if (tid == 0) {
+      L.cnt[0] = 0u;
+      L.cnt[1] = 0u;
+    }
+    __syncthreads();
+    for (int64_t i = tid; i < C; i += nt) part(cp[i]);
   }
   __syncthreads();
   const uint32_t nless = L.cnt[0];
@@ -174,17 +225,23 @@ SFM_DEV float exact_median(const float* Rp, int64_t n, const MedianState& s, uin
   if (tid == 0) L.cnt[0] = 0u;
   __syncthreads();
   const uint32_t b1 = s.bucket[0], b2 = s.bucket[1];
-  for (int64_t base = 0; base < n; base += nt) {
-    const int64_t i = base + tid;
-    uint32_t key = 0;
-    bool in = false;
-    if (i < n) {
-      key = fkey(Rp[i]);
-      const uint32_t d = key >> (32 - kMedBits1);
-      in = d == b1 || d == b2;
+  constexpr int U = 8;  // loads in flight per thread
+  for (int64_t base = 0; base < n; base += (int64_t)nt * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + tid + (int64_t)nt * u;
+      v[u] = i < n ? Rp[i] : 0.0f;
     }
-    const int slot = lds_wave_append(&L.cnt[0], in);
-    if (in) list[slot] = key;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = base + tid + (int64_t)nt * u;
+      const uint32_t key = fkey(v[u]);
+      const uint32_t d = key >> (32 - kMedBits1);
+      const bool in = i < n && (d == b1 || d == b2);
+      const int slot = lds_wave_append(&L.cnt[0], in);
+      if (in) list[slot] = key;
+    }
   }
   __syncthreads();
   const int64_t m = (int64_t)L.cnt[0];
@@ -205,6 +262,46 @@ SFM_DEV int64_t exact_nms(const float* Rp, int H, int W, int kh, float med, uint
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
   if (tid == 0) L.cnt[1] = 0u;
   __syncthreads();
+  if (kh == 1) {
+    // 3 x 3: per row, four 64-column chunks with all their loads in flight together; the
+    // column maxima's left / right neighbours come from the adjacent lanes (the chunk's edge
+    // lanes load theirs); out-of-image cells are -inf, so v == window max <=> none larger
+    constexpr int NCH = 4;
+    for (int y = wid; y < H; y += nw) {
+      for (int xb = 0; xb < W; xb += 64 * NCH) {
+        float c[NCH][3], e[NCH][3];
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+          const int x = xb + 64 * ch + lane;
+          const int xe = lane == 0 ? x - 1 : x + 1;  // edge lanes: the column beyond the chunk
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy) {
+            const int yy = y + dy - 1;
+            const bool rok = yy >= 0 && yy < H;
+            c[ch][dy] = (rok && x < W) ? Rp[(int64_t)yy * W + x] : -INFINITY;
+            e[ch][dy] = (rok && (lane == 0 || lane == 63) && xe >= 0 && xe < W) ? Rp[(int64_t)yy * W + xe] : -INFINITY;
+          }
+        }
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+          const int x = xb + 64 * ch + lane;
+          const float cm = fmaxf(fmaxf(c[ch][0], c[ch][1]), c[ch][2]);
+          const float em = fmaxf(fmaxf(e[ch][0], e[ch][1]), e[ch][2]);
+          const float up = __shfl_up(cm, 1), dn = __shfl_down(cm, 1);
+          const float l = lane == 0 ? em : up, r = lane == 63 ? em : dn;
+          const float v = c[ch][1];
+          const float m = fmaxf(fmaxf(l, cm), r);
+          const bool pred = x < W && ((v < med) ? (v == 0.0f) : (v == m));  // :92, :95
+          const int slot = lds_wave_append(&L.cnt[1], pred);
+          if (pred) cp[slot] = ((uint64_t)(~fkey(v)) << 32) | (uint32_t)(y * W + x);
+        }
+      }
+    }
+    __syncthreads();
+    const int64_t C = (int64_t)L.cnt[1];
+    __syncthreads();
+    return C;
+  }
   for (int y = wid; y < H; y += nw) {
     const int y0 = max(y - kh, 0), y1 = min(y + kh, H - 1);
     for (int xb = 0; xb < W; xb += 64) {
