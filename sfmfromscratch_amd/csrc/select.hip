@@ -217,6 +217,44 @@ SFM_DEV int lds_wave_append(uint32_t* counter, bool pred) {
   return pred ? (int)(base + (uint32_t)__popcll(lower)) : -1;
 }
 
+// Both middle keys from the collected list at once: digit 2 (11 bits) of rank r1 in bucket b1
+// and of rank r2 in bucket b2 histogrammed in the two halves of s_h in one list pass, then
+// digit 3 (10 bits) likewise (as select_in_list twice, in half the passes).
+SFM_DEV void select_pair_in_list(const uint32_t* lp, int64_t m, uint32_t b1, uint32_t r1, uint32_t b2, uint32_t r2,
+                                 const SelectLds& L, uint32_t* key1, uint32_t* key2) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int i = tid; i < kHistBins; i += nt) L.h[i] = 0u;
+  __syncthreads();
+  for (int64_t i = tid; i < m; i += nt) {
+    const uint32_t k = lp[i];
+    if ((k >> 21) == b1) atomicAdd(&L.h[(k >> 10) & 0x7ffu], 1u);
+    if ((k >> 21) == b2) atomicAdd(&L.h[2048 + ((k >> 10) & 0x7ffu)], 1u);
+  }
+  __syncthreads();
+  find_bin(L.h, 2048, r1, L.scan, L.out);
+  const uint32_t pre1 = (b1 << 11) | L.out[0];
+  r1 -= L.out[1];
+  __syncthreads();
+  find_bin(L.h + 2048, 2048, r2, L.scan, L.out);
+  const uint32_t pre2 = (b2 << 11) | L.out[0];
+  r2 -= L.out[1];
+  __syncthreads();
+  for (int i = tid; i < 2048; i += nt) L.h[i] = 0u;
+  __syncthreads();
+  for (int64_t i = tid; i < m; i += nt) {
+    const uint32_t k = lp[i];
+    if ((k >> 10) == pre1) atomicAdd(&L.h[k & 0x3ffu], 1u);
+    if ((k >> 10) == pre2) atomicAdd(&L.h[1024 + (k & 0x3ffu)], 1u);
+  }
+  __syncthreads();
+  find_bin(L.h, 1024, r1, L.scan, L.out);
+  *key1 = (pre1 << 10) | L.out[0];
+  __syncthreads();
+  find_bin(L.h + 1024, 1024, r2, L.scan, L.out);
+  *key2 = (pre2 << 10) | L.out[0];
+  __syncthreads();
+}
+
 // np.median of the plane (NaiveSIFT.py:91): the keys of the two digit-1 buckets holding the
 // middle ranks (from the Harris histogram's select scan) are collected into `list`, then
 // digits 2 and 3 resolved by select_in_list.  Even n: float32 (v[n/2-1] + v[n/2]) / 2.
@@ -246,84 +284,89 @@ SFM_DEV float exact_median(const float* Rp, int64_t n, const MedianState& s, uin
   __syncthreads();
   const int64_t m = (int64_t)L.cnt[0];
   __syncthreads();
-  const uint32_t key1 = select_in_list(list, m, b1, s.rank[0], L.h, L.scan, L.out);
+  if (s.odd) return fkey_inv(select_in_list(list, m, b1, s.rank[0], L.h, L.scan, L.out));
+  uint32_t key1, key2;
+  select_pair_in_list(list, m, b1, s.rank[0], b2, s.rank[1], L, &key1, &key2);
   const float v1 = fkey_inv(key1);
-  if (s.odd) return v1;
-  const uint32_t key2 = select_in_list(list, m, b2, s.rank[1], L.h, L.scan, L.out);
   const float v2 = fkey_inv(key2);
   const float sum = v1 + v2;
   return sum / 2.0f;
 }
 
-// The reference's NMS predicate with the exact median (nms.hip, mode 1): candidate <=>
-// (R >= med && no cell of the clipped (2kh+1)^2 window is larger) || (R < med && R == 0).
-// One wavefront per row; candidates appended to cp (any order: top-k orders them).
+// The reference's NMS predicate with the exact median, over one plane inside the workgroup
+// (nms.hip, mode 1): candidate <=> (R >= med && no cell of the clipped window is larger) ||
+// (R < med && R == 0) (:92, :95); appended to cp in any order (top-k orders them).
+// 3 x 3: wavefront rows of four 64-column chunks (RB rows per iteration), every load in
+// flight together; the column maxima's neighbours come from the adjacent lanes (the
+// chunk's edge lanes load theirs); out-of-image cells are -inf, so v == window max <=>
+// none larger.  Other windows: a clipped-window loop per pixel.
 SFM_DEV int64_t exact_nms(const float* Rp, int H, int W, int kh, float med, uint64_t* cp, const SelectLds& L) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
   if (tid == 0) L.cnt[1] = 0u;
   __syncthreads();
+  auto pred_of = [&](float v, float m) { return (v < med) ? (v == 0.0f) : (v == m); };
   if (kh == 1) {
-    // 3 x 3: per row, four 64-column chunks with all their loads in flight together; the
-    // column maxima's left / right neighbours come from the adjacent lanes (the chunk's edge
-    // lanes load theirs); out-of-image cells are -inf, so v == window max <=> none larger
-    constexpr int NCH = 4;
-    for (int y = wid; y < H; y += nw) {
+    constexpr int NCH = 4, RB = 1;
+    for (int y0 = wid * RB; y0 < H; y0 += nw * RB) {
       for (int xb = 0; xb < W; xb += 64 * NCH) {
-        float c[NCH][3], e[NCH][3];
+        float c[RB][NCH][3], e[RB][NCH][3];
 #pragma unroll
-        for (int ch = 0; ch < NCH; ++ch) {
-          const int x = xb + 64 * ch + lane;
-          const int xe = lane == 0 ? x - 1 : x + 1;  // edge lanes: the column beyond the chunk
+        for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-          for (int dy = 0; dy < 3; ++dy) {
-            const int yy = y + dy - 1;
-            const bool rok = yy >= 0 && yy < H;
-            c[ch][dy] = (rok && x < W) ? Rp[(int64_t)yy * W + x] : -INFINITY;
-            e[ch][dy] = (rok && (lane == 0 || lane == 63) && xe >= 0 && xe < W) ? Rp[(int64_t)yy * W + xe] : -INFINITY;
+          for (int ch = 0; ch < NCH; ++ch) {
+            const int y = y0 + rb;
+            const int x = xb + 64 * ch + lane;
+            const int xe = lane == 0 ? x - 1 : x + 1;  // edge lanes: the column beyond the chunk
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) {
+              const int yy = y + dy - 1;
+              const bool rok = yy >= 0 && yy < H && y < H;
+              c[rb][ch][dy] = (rok && x < W) ? Rp[(int64_t)yy * W + x] : -INFINITY;
+              e[rb][ch][dy] =
+                  (rok && (lane == 0 || lane == 63) && xe >= 0 && xe < W) ? Rp[(int64_t)yy * W + xe] : -INFINITY;
+            }
           }
-        }
 #pragma unroll
-        for (int ch = 0; ch < NCH; ++ch) {
-          const int x = xb + 64 * ch + lane;
-          const float cm = fmaxf(fmaxf(c[ch][0], c[ch][1]), c[ch][2]);
-          const float em = fmaxf(fmaxf(e[ch][0], e[ch][1]), e[ch][2]);
-          const float up = __shfl_up(cm, 1), dn = __shfl_down(cm, 1);
-          const float l = lane == 0 ? em : up, r = lane == 63 ? em : dn;
-          const float v = c[ch][1];
-          const float m = fmaxf(fmaxf(l, cm), r);
-          const bool pred = x < W && ((v < med) ? (v == 0.0f) : (v == m));  // :92, :95
-          const int slot = lds_wave_append(&L.cnt[1], pred);
-          if (pred) cp[slot] = ((uint64_t)(~fkey(v)) << 32) | (uint32_t)(y * W + x);
-        }
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+          for (int ch = 0; ch < NCH; ++ch) {
+            const int y = y0 + rb;
+            const int x = xb + 64 * ch + lane;
+            const float cm = fmaxf(fmaxf(c[rb][ch][0], c[rb][ch][1]), c[rb][ch][2]);
+            const float em = fmaxf(fmaxf(e[rb][ch][0], e[rb][ch][1]), e[rb][ch][2]);
+            const float up = __shfl_up(cm, 1), dn = __shfl_down(cm, 1);
+            const float l = lane == 0 ? em : up, r = lane == 63 ? em : dn;
+            const float v = c[rb][ch][1];
+            const bool pred = y < H && x < W && pred_of(v, fmaxf(fmaxf(l, cm), r));
+            const int slot = lds_wave_append(&L.cnt[1], pred);
+            if (pred) cp[slot] = ((uint64_t)(~fkey(v)) << 32) | (uint32_t)(y * W + x);
+          }
       }
     }
-    __syncthreads();
-    const int64_t C = (int64_t)L.cnt[1];
-    __syncthreads();
-    return C;
-  }
-  for (int y = wid; y < H; y += nw) {
-    const int y0 = max(y - kh, 0), y1 = min(y + kh, H - 1);
-    for (int xb = 0; xb < W; xb += 64) {
-      const int x = xb + lane;
-      bool pred = false;
-      float v = 0.0f;
-      if (x < W) {
-        v = Rp[(int64_t)y * W + x];
-        if (v < med) {
-          pred = v == 0.0f;  // R_maxpool[R < median] = 0 (:92)
-        } else {
-          const int x0 = max(x - kh, 0), x1 = min(x + kh, W - 1);
-          bool ismax = true;
-          for (int yy = y0; yy <= y1; ++yy) {
-            const float* row = Rp + (int64_t)yy * W;
-            for (int xx = x0; xx <= x1; ++xx) ismax &= !(row[xx] > v);
+  } else {
+    for (int y = wid; y < H; y += nw) {
+      const int y0 = max(y - kh, 0), y1 = min(y + kh, H - 1);
+      for (int xb = 0; xb < W; xb += 64) {
+        const int x = xb + lane;
+        bool pred = false;
+        float v = 0.0f;
+        if (x < W) {
+          v = Rp[(int64_t)y * W + x];
+          if (v < med) {
+            pred = v == 0.0f;  // R_maxpool[R < median] = 0 (:92)
+          } else {
+            const int x0 = max(x - kh, 0), x1 = min(x + kh, W - 1);
+            bool ismax = true;
+            for (int yy = y0; yy <= y1; ++yy) {
+              const float* row = Rp + (int64_t)yy * W;
+              for (int xx = x0; xx <= x1; ++xx) ismax &= !(row[xx] > v);
+            }
+            pred = ismax;
           }
-          pred = ismax;
         }
+        const int slot = lds_wave_append(&L.cnt[1], pred);
+        if (pred) cp[slot] = ((uint64_t)(~fkey(v)) << 32) | (uint32_t)(y * W + x);
       }
-      const int slot = lds_wave_append(&L.cnt[1], pred);
-      if (pred) cp[slot] = ((uint64_t)(~fkey(v)) << 32) | (uint32_t)(y * W + x);
     }
   }
   __syncthreads();
@@ -359,7 +402,7 @@ __global__ void __launch_bounds__(1024) k_select(const float* __restrict__ R, ui
     return;
   }
   if (!s.fallback) {
-    const int64_t C = (int64_t)cand_count[(int64_t)b * kCounterStride];
+    const int64_t C = (int64_t)cand_count[(int64_t)b * kCounterStride];  // certified NMS's candidates
     if (C >= (int64_t)k) {
       topk_sorted(cp, C, k, tp, L);
       if (~(uint32_t)(L.sel[k - 1] >> 32) >= s.tcert) {  // k-th candidate above the median's bucket
