@@ -290,16 +290,14 @@ __global__ void __launch_bounds__(NT) k_nms_stream(const float* __restrict__ R,
                                       s_wsum, &s_base);
     if (flags == 0) continue;
     uint64_t* out = cand + (int64_t)b * n + slot;
-  #pragma unroll
-    for (int i = 0; i < SH; ++i) {
-      if ((flags >> (4 * i)) & 0xFull) {
-        const float c[4] = {v[i + 1].x, v[i + 1].y, v[i + 1].z, v[i + 1].w};
-        const uint32_t rowidx = (uint32_t)((y0 + 1 + i) * W + 4 * c4);
-  #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if ((flags >> (4 * i + e)) & 1ull) *out++ = ((uint64_t)(~fkey(c[e])) << 32) | (rowidx + e);
-  }
-}
+    // the few candidates re-read their value (an L2 hit) instead of keeping the strip's
+    // rows live across the append: 156 -> fewer VGPRs, more workgroups per CU in flight
+    while (flags) {
+      const int bit = __builtin_ctzll(flags);
+      flags &= flags - 1;
+      const uint32_t idx = (uint32_t)((y0 + 1 + (bit >> 2)) * W + 4 * c4 + (bit & 3));
+      *out++ = ((uint64_t)(~fkey(Rp[idx])) << 32) | idx;
+    }
   }
 }
 
