@@ -55,6 +55,30 @@ PEAK_MATCH_TFLOPS = 2500.0 / 3
 HARRIS_FLOP_PER_PX = 328   # Sobel 2x6 fma (24) + 3 products + 3x49 fma (294) + R (7)
 MATCH_FLOP_PER_ELEM = 2    # GEMM-equivalent: one multiply-add per descriptor element pair
 DESC_BYTES_PER_KP = 20 * 20 * 4 + 128 * 4 + 12   # level window + halo read, descriptor + xy/conf written
+# Describe (k_describe_q): modelled algorithmic lane-ops per keypoint at window width ws
+#  against the FP32 lane-op rate (1024 SIMDs x 16 lanes x 2.4 GHz; the
+# orientation sort's float64 min/max count twice, the f64 vector rate being half).
+VALU_LANE_OPS = 1024 * 16 * 2.4e9
+
+
+def describe_ops(ws: int) -> float:
+    """Lane-ops per keypoint of the reference's describe at window width ws
+    (ScaleRotInvSIFT.py:33-87): per pixel Sobel (2 x 6 fma), |g| (4) and atan2 (~28); the
+    bitwise-exact np.histogram path sorts the ws*ws orientation keys (bitonic, P = pow2 >= N,
+    4 slots per f64 compare-exchange), a prefix sum and 37 bin-edge searches; 16 cells each
+    sort, prefix-sum and bin their pixels; 128-D normalise + sqrt (RootSIFT)."""
+    import math
+    n = ws * ws
+    p = max(1 << max(0, math.ceil(math.log2(n))), 16)
+    lg = int(math.log2(p))
+    ops = 44.0 * n + 4.0 * (p // 2) * lg * (lg + 1) / 2 + n + 37 * math.ceil(math.log2(n + 1))
+    c = max(1, n // 16)
+    pc = 1 << math.ceil(math.log2(c)) if c > 1 else 1
+    lc = int(math.log2(pc))
+    ops += 16 * (2.0 * (pc // 2) * lc * (lc + 1) / 2 + c + 9 * math.ceil(math.log2(c + 1)))
+    return ops + 128 * 4
+
+
 KERNELS = {"harris": "k_harris<7>", "match": "k_match_mfma", "describe": "k_describe_q",
            "nms": "k_nms_stream<8,256>", "median": "k_med_scan", "topk": "k_topk", "pyramid": "k_down2x3",
            "match_prep": "k_match_prep", "match_post": "k_match_compact"}
@@ -269,6 +293,27 @@ def main():
             "pyramid": ("hbm", pyr_bytes / 1e9, "GB/s", PEAK_HBM_GBS, pyr_bytes),
         }
 
+    def level_keypoints():
+        """Keypoints per pyramid level over the batch (host-path extraction of the same frames,
+        outside every timed region): the describe floor's keypoint counts."""
+        if args.rgb_ingest:
+            return None
+        from sfmfromscratch_amd import _native, _abi
+        ctx = _native.Context(_abi.params_from_dict(P_OCT, _abi.SFM_MODE_SCALEROT), device=dev.index)
+        tot = np.zeros(P_OCT["pyramid_level"], np.int64)
+        host = frames.cpu().numpy()
+        for i in range(B):
+            tot += ctx.extract(host[i])[4]
+        ctx.close()
+        return tot
+
+    def describe_floor(lvl_kp, nsteps):
+        """(floor ms, modelled lane-ops) of the describe stage over nsteps steps."""
+        fws = [max(3, int(P_OCT["feature_width"] / (P_OCT["pyramid_scale_factor"] ** l)))
+               for l in range(P_OCT["pyramid_level"])]
+        ops = sum(int(k) * describe_ops(2 * (fw // 2)) for k, fw in zip(lvl_kp, fws)) * nsteps
+        return ops / VALU_LANE_OPS * 1e3, ops
+
     def prof_enable(on):
         for c in ctxs:
             c.profile_enable(on)
@@ -307,6 +352,15 @@ def main():
                 ach = amount / (ms / 1e3)
                 st.update({"bound": bound, "achieved": round(ach, 3), "unit": unit, "frac": round(ach / peak, 4)})
             stages[k] = st
+        lvl_kp = level_keypoints()
+        if lvl_kp is not None and "describe" in stages:
+            fl_ms, ops = describe_floor(lvl_kp, nprof)
+            d = stages["describe"]
+            d.update({"bound": "valu", "achieved": round(ops / (prof_all["describe"][0] / 1e3) / 1e12, 3),
+                      "unit": "T lane-op/s", "floor_ms_per_step": round(fl_ms / nprof, 4),
+                      "frac": round(fl_ms / prof_all["describe"][0], 4),
+                      "keypoints_per_level": [int(v) for v in lvl_kp],
+                      "note": "modelled lane-ops per keypoint (bench.describe_ops) / 39.3 T lane-op/s"})
         dom = max((k for k in prof_all if k in work and prof_all[k][1]), key=lambda k: prof_all[k][0])
         for c in ctxs:
             c.profile_stages([dom])

@@ -3,7 +3,7 @@
 // window sums -> R = det - alpha * trace^2, plus the first radix digit histogram of R
 // for the exact median (NaiveSIFT.py:91).
 //
-// One workgroup (256 threads) walks 64 x 64 output tiles of one plane (see k_harris).  The
+// One workgroup walks 64 x 64 output tiles of one plane (see k_harris).  The
 // 2-D window is the reference's full KS x KS correlation (not separable: a separable sum
 // would round differently and move keypoints), accumulated per pixel as an
 // fma chain in row-major tap order (OpenCV FilterVec_32f's v_muladd chain; DESIGN.md
@@ -44,7 +44,7 @@ __device__ __forceinline__ void pk_fma_bcast(f32x2& acc, f32x2 k, f32x2 v) {
     asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(k), "v"(v));
 }
 
-// One workgroup (256 threads, 4 waves, 2 per CU) walks 64 x 64 output tiles of one plane.
+// One workgroup (2 per CU; see HarrisShape) walks 64 x 64 output tiles of one plane.
 // LDS holds the image tile (+ Sobel and window halo) and the two gradient planes Ix, Iy of
 // the tile + window halo.  Each thread owns 4 columns x 4 rows: for every LDS gradient row
 // it forms the three products Ix^2, Iy^2, IxIy in registers (v_pk_mul_f32; the same IEEE
@@ -64,8 +64,19 @@ __device__ __forceinline__ void pk_fma_bcast(f32x2& acc, f32x2 k, f32x2 v) {
 constexpr int kStampSlots = 48;
 __device__ uint64_t* g_harris_stamps;
 
-template <int KS, bool VEC, int ABL = 0>
-__global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float* __restrict__ gk, float alpha) {
+// NPAIR: output row pairs per thread.  2: 256 threads x (4 columns x 4 rows), 2 waves per
+// SIMD at up to 256 VGPRs.  1: 512 threads x (4 columns x 2 rows), 4 waves per SIMD at up to
+// 128 VGPRs (the window's packed fmas issue faster at 4 waves per SIMD), at
+// the price of each gradient row's products being formed by twice as many threads.
+template <int NPAIR>
+struct HarrisShape {
+  static constexpr int NT = 512 / NPAIR;   // threads per workgroup (2 workgroups per CU: NT / 128 waves per SIMD)
+  static constexpr int RPT = 2 * NPAIR;    // output rows per thread
+};
+
+template <int KS, bool VEC, int ABL = 0, int NPAIR = 2>
+__global__ void __launch_bounds__(HarrisShape<NPAIR>::NT, HarrisShape<NPAIR>::NT / 128) k_harris(HarrisLevels lvs, const float* __restrict__ gk, float alpha) {
+  constexpr int NT = HarrisShape<NPAIR>::NT, RPT = HarrisShape<NPAIR>::RPT;
   // this workgroup's level (one launch may hold several pyramid levels: the small levels'
   // tiles share a launch instead of each paying a launch and a tail)
   int li = 0;
@@ -83,9 +94,11 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
   constexpr int NV4 = (NV + 3) / 4;         // b128 LDS loads per row per plane
   constexpr int NVP = 4 * NV4;
   constexpr int NP2 = (NV + 1) / 2;         // product pairs per row
-  // gradient row stride == 8 (mod 32) floats: a 16-lane group of a ds_read_b128 holds
-  // 8 column groups x 2 row quads, whose 16-B chunks 8*rq + tq (mod 16) are distinct
-  constexpr int PWP = (kHT + KS - 1 <= 72 && 60 + NVP <= 72) ? 72 : ((60 + NVP <= 104) ? 104 : 136);
+  // a 16-lane group of a ds_read_b128 holds 8 column groups x 2 row groups (RPT rows apart):
+  // RPT * stride / 4 == 8 (mod 16) 16-B chunks keeps the chunks 8*rq + tq (mod 16) distinct,
+  // i.e. stride == 8 (mod 32) floats for RPT 4 and == 16 (mod 32) for RPT 2
+  constexpr int PWP = RPT == 4 ? ((kHT + KS - 1 <= 72 && 60 + NVP <= 72) ? 72 : ((60 + NVP <= 104) ? 104 : 136))
+                               : ((kHT + KS - 1 <= 80 && 60 + NVP <= 80) ? 80 : ((60 + NVP <= 112) ? 112 : 144));
   static_assert(PWP >= kHT + KS - 1 && 60 + NVP <= PWP, "harris LDS row stride");
   constexpr int NS = PWP / 4;               // 4-wide gradient strips per row
   constexpr int XA = (GA + 1 + 3) / 4 * 4;  // image tile margin left of the output tile
@@ -94,14 +107,14 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
   constexpr int IH = PH + 2;                // image tile rows (Sobel halo)
   constexpr int IWP = PWP + 4 * (NR4 - 1);  // covers every strip's reads
   constexpr int IW4 = IWP / 4;
-  constexpr int NIMG = VEC ? (IH * IW4 + 255) / 256 : (IH * IWP + 255) / 256;
+  constexpr int NIMG = VEC ? (IH * IW4 + NT - 1) / NT : (IH * IWP + NT - 1) / NT;
   static_assert(NIMG <= 64, "prefetch mask");
   __shared__ __attribute__((aligned(16))) float s_g[2][PH][PWP];
   __shared__ __attribute__((aligned(16))) float s_img[IH][IWP];
   __shared__ uint32_t s_hist[kMedBins1];  // digit-1 histogram, flushed once per workgroup
   // tap pairs per gradient row r and row pair p: (g[r-2p][j], g[r-2p-1][j]), 0 where the
   // tap row does not exist; read as uniform LDS broadcasts (49 taps in SGPRs spill)
-  __shared__ __attribute__((aligned(16))) f32x2 s_tp[KS + 3][2][KS + (KS & 1)];
+  __shared__ __attribute__((aligned(16))) f32x2 s_tp[KS + 2 * NPAIR - 1][NPAIR][KS + (KS & 1)];
   __shared__ uint32_t s_last, s_red[8];
 
   const int tid = threadIdx.x;
@@ -117,15 +130,15 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
   }
   const float* img = lvl + (int64_t)b * H * W;
   float* Rp = Rout + (int64_t)b * H * W;
-  for (int i = tid; i < kMedBins1; i += 256) s_hist[i] = 0u;
-  for (int i = tid; i < (KS + 3) * 2 * KS; i += 256) {
-    const int r = i / (2 * KS), p = (i / KS) & 1, j = i % KS;
+  for (int i = tid; i < kMedBins1; i += NT) s_hist[i] = 0u;
+  for (int i = tid; i < (KS + 2 * NPAIR - 1) * NPAIR * KS; i += NT) {
+    const int r = i / (NPAIR * KS), p = (i / KS) % NPAIR, j = i % KS;
     const int i0 = r - 2 * p, i1 = i0 - 1;
     s_tp[r][p][j] = f32x2{(i0 >= 0 && i0 < KS) ? gk[i0 * KS + j] : 0.0f, (i1 >= 0 && i1 < KS) ? gk[i1 * KS + j] : 0.0f};
   }
   const int lane = tid & 63, wv = tid >> 6;
   const int tq = (lane & 7) | ((wv & 1) << 3);          // columns 4tq .. 4tq+3
-  const int rq = ((lane >> 3) & 7) | ((wv >> 1) << 3);  // rows 4rq .. 4rq+3
+  const int rq = ((lane >> 3) & 7) | ((wv >> 1) << 3);  // rows RPT*rq .. RPT*rq+RPT-1
 
   // image tile of `tile` -> registers (zero outside the image = BORDER_CONSTANT)
   typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -139,7 +152,7 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
     if constexpr (VEC) {
 #pragma unroll
       for (int k = 0; k < NIMG; ++k) {
-        const int e = tid + 256 * k;
+        const int e = tid + NT * k;
         const int iy = e / IW4, gx = gx0 + 4 * (e - iy * IW4), gy = gy0 + iy;
         const bool ok = e < IH * IW4 && gy >= 0 && gy < H && gx >= 0 && gx < W;
         const int64_t off = ok ? (int64_t)gy * W + gx : 0;
@@ -149,7 +162,7 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
     } else {
 #pragma unroll
       for (int k = 0; k < NIMG; ++k) {
-        const int e = tid + 256 * k;
+        const int e = tid + NT * k;
         const int iy = e / IWP, gx = gx0 + (e - iy * IWP), gy = gy0 + iy;
         const bool ok = e < IH * IWP && gy >= 0 && gy < H && gx >= 0 && gx < W;
         t1[k] = img[ok ? (int64_t)gy * W + gx : 0];
@@ -167,11 +180,11 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
     for (int k = 0; k < NIMG; ++k) {
       const bool ok = (okmask >> k) & 1ull;
       if constexpr (VEC) {
-        const int e = tid + 256 * k;
+        const int e = tid + NT * k;
         if (e < IH * IW4)
           reinterpret_cast<f32x4*>(&s_img[0][0])[e] = ok ? t4[k] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
       } else {
-        const int e = tid + 256 * k;
+        const int e = tid + NT * k;
         if (e < IH * IWP) (&s_img[0][0])[e] = ok ? t1[k] : 0.0f;
       }
     }
@@ -185,7 +198,7 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
     //    (each half an IEEE fma, as the scalar chain); interior tiles skip the masking.
     auto sobel = [&](auto maskedc) {
       constexpr bool MASKED = decltype(maskedc)::value;
-      for (int sidx = tid; sidx < PH * NS; sidx += 256) {
+      for (int sidx = tid; sidx < PH * NS; sidx += NT) {
         const int py = sidx / NS, px0 = (sidx - py * NS) * 4;
         f32x2 w[3][2 * NR4];
 #pragma unroll
@@ -274,20 +287,20 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
     //    order.  acc[p][pl][q] = (row 4rq+2p, row 4rq+2p+1) at column 4tq+q; gradient row
     //    4rq+r feeds tap row r-2p of the pair's first row and r-2p-1 of its second: packed
     //    fmas where both are taps, a scalar fma on one half at the pair's first/last row.
-    f32x2 acc[2][3][4];
+    f32x2 acc[NPAIR][3][4];
 #pragma unroll
-    for (int p = 0; p < 2; ++p)
+    for (int p = 0; p < NPAIR; ++p)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[p][pl][q] = f32x2{0.0f, 0.0f};
-    constexpr int NR = (ABL == 2) ? 1 : KS + 3;  // gradient rows feeding this thread
+    constexpr int NR = (ABL == 2) ? 1 : KS + 2 * NPAIR - 1;  // gradient rows feeding this thread
     static_for<NR>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
       f32x2 P[3][NP2];
       {
-        const float4* rx = reinterpret_cast<const float4*>(&s_g[0][4 * rq + r][4 * tq]);
-        const float4* ry = reinterpret_cast<const float4*>(&s_g[1][4 * rq + r][4 * tq]);
+        const float4* rx = reinterpret_cast<const float4*>(&s_g[0][RPT * rq + r][4 * tq]);
+        const float4* ry = reinterpret_cast<const float4*>(&s_g[1][RPT * rq + r][4 * tq]);
         f32x2 X[NVP / 2], Y[NVP / 2];
 #pragma unroll
         for (int c4 = 0; c4 < NV4; ++c4) {
@@ -304,9 +317,9 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
           P[2][m] = X[m] * Y[m];
         }
       }
-      f32x2 T[2][KS + (KS & 1)];
+      f32x2 T[NPAIR][KS + (KS & 1)];
 #pragma unroll
-      for (int p = 0; p < 2; ++p)
+      for (int p = 0; p < NPAIR; ++p)
 #pragma unroll
         for (int j2 = 0; j2 < (KS + 1) / 2; ++j2) {
           const float4 t = *reinterpret_cast<const float4*>(&s_tp[r][p][2 * j2]);
@@ -314,7 +327,7 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
           T[p][2 * j2 + 1] = f32x2{t.z, t.w};
         }
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
+      for (int p = 0; p < NPAIR; ++p) {
         const int i0 = r - 2 * p, i1 = r - 2 * p - 1;  // tap rows of the pair's two rows
         const bool v0 = i0 >= 0 && i0 < KS && (ABL != 2 || i0 == 0);
         const bool v1 = i1 >= 0 && i1 < KS && ABL != 2;
@@ -340,8 +353,8 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
     // 3. R = det - alpha * trace^2 (:71-74), digit-1 histogram of R, R stored as 16-B
     //    row segments (a wave writes 8 rows x 128 contiguous bytes per store)
 #pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      const int gy = ty0 + 4 * rq + o;
+    for (int o = 0; o < RPT; ++o) {
+      const int gy = ty0 + RPT * rq + o;
       const int gx0 = tx0 + 4 * tq;
       float Rq[4];
 #pragma unroll
@@ -381,7 +394,7 @@ __global__ void __launch_bounds__(256, 2) k_harris(HarrisLevels lvs, const float
   }
   __syncthreads();
   uint32_t* hg = hist_g + (int64_t)b * kMedBins1;
-  for (int i = tid; i < kMedBins1; i += 256) {
+  for (int i = tid; i < kMedBins1; i += NT) {
     uint32_t c = s_hist[i];
     if (c) atomicAdd(&hg[i], c);
   }
@@ -422,6 +435,15 @@ static int harris_plan(HarrisLevels& g, int B) {
   return wg;
 }
 
+// SFMFEAT_HARRIS_NPAIR=1|2: output row pairs per thread (A/B timing; see HarrisShape)
+static int harris_npair() {
+  static const int v = [] {
+    const char* e = getenv("SFMFEAT_HARRIS_NPAIR");
+    return (e && atoi(e) == 1) ? 1 : 2;
+  }();
+  return v;
+}
+
 template <int KS, int ABL = 0>
 static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipStream_t st) {
   bool vec = true;
@@ -431,10 +453,19 @@ static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipSt
     vec = vec && (g.l[k].W & 3) == 0;
   }
   const int nwg = harris_plan(g, B);
-  if (vec)
-    hipLaunchKernelGGL((k_harris<KS, true, ABL>), dim3(nwg, B), dim3(256), 0, st, g, gk, alpha);
-  else
-    hipLaunchKernelGGL((k_harris<KS, false, ABL>), dim3(nwg, B), dim3(256), 0, st, g, gk, alpha);
+  if (harris_npair() == 1) {
+    constexpr int NT = HarrisShape<1>::NT;
+    if (vec)
+      hipLaunchKernelGGL((k_harris<KS, true, ABL, 1>), dim3(nwg, B), dim3(NT), 0, st, g, gk, alpha);
+    else
+      hipLaunchKernelGGL((k_harris<KS, false, ABL, 1>), dim3(nwg, B), dim3(NT), 0, st, g, gk, alpha);
+  } else {
+    constexpr int NT = HarrisShape<2>::NT;
+    if (vec)
+      hipLaunchKernelGGL((k_harris<KS, true, ABL, 2>), dim3(nwg, B), dim3(NT), 0, st, g, gk, alpha);
+    else
+      hipLaunchKernelGGL((k_harris<KS, false, ABL, 2>), dim3(nwg, B), dim3(NT), 0, st, g, gk, alpha);
+  }
 }
 
 void launch_harris_levels(const HarrisLevels& g, int B, const float* d_gauss, int ks, float alpha, hipStream_t st) {

@@ -50,17 +50,20 @@ constexpr uint32_t kHugeBucket = 0x7F4u;
 
 // Per-plane select scan (median.hip k_med_scan; fused into the Harris kernel's last
 // workgroup of each plane): from the digit-1 histogram, the buckets holding the two
-// middle ranks (exact-median state) and the certified-select thresholds.  Needs exactly
-// 256 threads (8 bins each, one prefix pass for all three ranks); s_red holds 8 u32.
+// middle ranks (exact-median state) and the certified-select thresholds.  Needs 256 or
+// 512 threads (8 bins each for the first 256, one prefix pass for all three ranks); s_red
+// holds 8 u32.
 // `hist` is read with agent-scope atomic loads so a fused caller sees every workgroup's
 // flush (L2 is per XCD); the 8 loads per thread are issued together.
 SFM_DEV void select_scan_plane(const uint32_t* hist, MedianState* st, unsigned long long* list_count,
                                int64_t n, int64_t vmin, int force_exact, uint32_t* s_red) {
   static_assert(kMedBins1 == 256 * 8, "select scan: 8 bins per thread");
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const bool act = tid < 256;  // a 512-thread caller: the upper half holds no bins
   uint32_t v[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = __hip_atomic_load(hist + 8 * tid + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int j = 0; j < 8; ++j)
+    v[j] = act ? __hip_atomic_load(hist + 8 * tid + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
   uint32_t local = 0;
 #pragma unroll
   for (int j = 0; j < 8; ++j) local += v[j];
