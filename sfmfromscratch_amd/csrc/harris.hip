@@ -171,7 +171,18 @@ __global__ void __launch_bounds__(HarrisShape<NPAIR>::NT, HarrisShape<NPAIR>::NT
     }
   };
   if (wgx < ntiles) prefetch(wgx);
+  const int tmax = (ntiles + nwg - 1) / nwg;  // tiles of the busiest workgroup
   for (int tile = wgx; tile < ntiles; tile += nwg) {
+    if (lvs.prio) {
+      // the two workgroups resident on a CU share its SIMDs; the arbiter favours the older
+      // waves, so one runs ahead and the other finishes alone.  A workgroup with more tiles
+      // left issues at a higher priority, which keeps the two level.
+      const int left = (ntiles - tile + nwg - 1) / nwg;
+      if (4 * left > 3 * tmax) __builtin_amdgcn_s_setprio(3);
+      else if (2 * left > tmax) __builtin_amdgcn_s_setprio(2);
+      else if (4 * left > tmax) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
     const int tx0 = (tile % tiles_x) * kHT;
     const int ty0 = (tile / tiles_x) * kHT;
     __syncthreads();  // the previous tile's LDS reads are done
@@ -446,6 +457,11 @@ static int harris_npair() {
 
 template <int KS, int ABL = 0>
 static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipStream_t st) {
+  static const int prio = [] {  // SFMFEAT_HARRIS_PRIO=1: tile-balancing issue priority (A/B)
+    const char* e = getenv("SFMFEAT_HARRIS_PRIO");
+    return e ? atoi(e) : 0;
+  }();
+  g.prio = prio;
   bool vec = true;
   for (int k = 0; k < g.n; ++k) {
     g.l[k].tiles_x = (g.l[k].W + kHT - 1) / kHT;

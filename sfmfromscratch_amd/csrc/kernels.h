@@ -210,6 +210,7 @@ struct HarrisLevels {
     SelectScan scan;
   } l[kHarrisMaxLevels];
   int n;
+  int prio;  // 1: waves raise their issue priority with the tiles they have left (A/B)
 };
 void launch_harris_levels(const HarrisLevels& g, int B, const float* d_gauss, int ks, float alpha,
                           hipStream_t st);
@@ -244,6 +245,23 @@ size_t describe_lds_bytes(int fw, int rotate);
 void launch_select(const float* R, uint64_t* cand, const unsigned long long* cand_count, uint32_t* medlist,
                    uint64_t* scratch, KpList kp, int kcap, int k, int B, int H, int W, int ksize, int half_window,
                    MedianState* state, hipStream_t st);
+// Several levels' selections in one launch (B workgroups per level, level-major); each
+// level brings its own medlist / scratch regions (they must not overlap).
+constexpr int kSelectMaxLevels = 4;
+struct SelectLevels {
+  struct Level {
+    const float* R;
+    uint64_t* cand;
+    const unsigned long long* cand_count;
+    uint32_t* medlist;
+    uint64_t* scratch;
+    KpList kp;
+    MedianState* state;
+    int H, W, hw;
+  } l[kSelectMaxLevels];
+  int n;
+};
+void launch_select_levels(const SelectLevels& g, int kcap, int k, int B, int ksize, hipStream_t st);
 
 // describe_q.hip: four keypoints per wavefront for window widths 2..22 (false: not handled)
 // out_count (the last level's launch): also write each slot's keypoint count

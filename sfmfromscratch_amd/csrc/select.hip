@@ -375,11 +375,18 @@ SFM_DEV int64_t exact_nms(const float* Rp, int H, int W, int kh, float med, uint
   return C;
 }
 
-__global__ void __launch_bounds__(1024) k_select(const float* __restrict__ R, uint64_t* __restrict__ cand,
-                                                 const unsigned long long* __restrict__ cand_count,
-                                                 uint32_t* __restrict__ medlist, uint64_t* __restrict__ scratch,
-                                                 KpList kp, int kcap, int k, int H, int W, int kh, int hw,
-                                                 MedianState* __restrict__ state) {
+__global__ void __launch_bounds__(1024) k_select(SelectLevels g, int kcap, int k, int kh, int B) {
+  // this workgroup's level and plane (levels are B workgroups each, level-major)
+  const int li = (int)blockIdx.x / B;
+  const SelectLevels::Level& lv = g.l[li];
+  const float* __restrict__ R = lv.R;
+  uint64_t* __restrict__ cand = lv.cand;
+  const unsigned long long* __restrict__ cand_count = lv.cand_count;
+  uint32_t* __restrict__ medlist = lv.medlist;
+  uint64_t* __restrict__ scratch = lv.scratch;
+  const KpList kp = lv.kp;
+  MedianState* __restrict__ state = lv.state;
+  const int H = lv.H, W = lv.W, hw = lv.hw;
   extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
   __shared__ uint32_t s_out[2];
   __shared__ uint32_t s_cnt[2];
@@ -392,7 +399,7 @@ __global__ void __launch_bounds__(1024) k_select(const float* __restrict__ R, ui
   L.cnt = s_cnt;
 
   const int tid = threadIdx.x;
-  const int b = blockIdx.x;
+  const int b = (int)blockIdx.x - li * B;
   const int64_t n = (int64_t)H * W;
   uint64_t* cp = cand + (int64_t)b * n;
   uint64_t* tp = scratch + (int64_t)b * n;
@@ -429,11 +436,18 @@ size_t topk_lds_bytes() {
   return (size_t)kTopkLdsCap * 8 + (size_t)kTieLdsCap * 8 + (size_t)kHistBins * 4 + 1024 * 4;
 }
 
+void launch_select_levels(const SelectLevels& g, int kcap, int k, int B, int ksize, hipStream_t st) {
+  if (g.n < 1 || g.n > kSelectMaxLevels || B < 1) return;
+  hipLaunchKernelGGL(k_select, dim3(B * g.n), dim3(1024), topk_lds_bytes(), st, g, kcap, k, ksize / 2, B);
+}
+
 void launch_select(const float* R, uint64_t* cand, const unsigned long long* cand_count, uint32_t* medlist,
                    uint64_t* scratch, KpList kp, int kcap, int k, int B, int H, int W, int ksize, int half_window,
                    MedianState* state, hipStream_t st) {
-  hipLaunchKernelGGL(k_select, dim3(B), dim3(1024), topk_lds_bytes(), st, R, cand, cand_count, medlist, scratch, kp,
-                     kcap, k, H, W, ksize / 2, half_window, state);
+  SelectLevels g{};
+  g.n = 1;
+  g.l[0] = SelectLevels::Level{R, cand, cand_count, medlist, scratch, kp, state, H, W, half_window};
+  launch_select_levels(g, kcap, k, B, ksize, st);
 }
 
 void init_topk_attributes() {

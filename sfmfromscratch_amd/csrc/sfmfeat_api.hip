@@ -390,7 +390,28 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     }
     l0 = l1;
   }
-  for (int l = L_aux; l < L; ++l) select_level(l, st);
+  // the caller stream's levels: one selection launch for all of them (each level its own
+  // scratch regions inside the stream's half), unless SFMFEAT_SELECT_MERGE=0
+  static const bool merge_select = [] {
+    const char* e = getenv("SFMFEAT_SELECT_MERGE");
+    return !(e && atoi(e) == 0);
+  }();
+  if (merge_select && L - L_aux > 1 && L - L_aux <= kSelectMaxLevels) {
+    StageScope sc(c, SFM_PROF_TOPK, st);
+    SelectLevels g{};
+    g.n = L - L_aux;
+    int64_t so = L_aux > 0 ? (int64_t)B * H * W : 0;
+    for (int l = L_aux; l < L; ++l) {
+      const LevelBufs& e = lb[l];
+      g.l[l - L_aux] = SelectLevels::Level{e.R, e.cand, candcnt + e.co, as<uint32_t>(c->d_medlist) + so,
+                                           as<uint64_t>(c->d_scratch) + so, e.kp, e.med, lv[l].h, lv[l].w,
+                                           lv[l].fw / 2};
+      so += (int64_t)B * lv[l].h * lv[l].w;
+    }
+    launch_select_levels(g, std::max(c->kcap, 1), c->kcap, B, c->p.ksize, st);
+  } else {
+    for (int l = L_aux; l < L; ++l) select_level(l, st);
+  }
   if (L_aux > 0 && L > L_aux) HIPCHK(c, hipStreamWaitEvent(st, c->ev[L + 2], 0));
   for (int l = L_aux; l < L; ++l) describe_level(l, st);
   // join: the caller's stream waits for the aux work

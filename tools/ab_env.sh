@@ -11,6 +11,6 @@ for rep in 1 2; do
     tail -1 gpurun_out/ab_${i}_$rep.log | python -c '
 import json,sys
 d=json.loads(sys.stdin.read()); st=d.get("stages_ms",{})
-print(sys.argv[1], d["value"], d["ms_per_step"], "frac", (d.get("roofline") or {}).get("frac"), " ".join(f"{k}={v[\"ms_per_step\"]}" for k,v in st.items()))' "$e"
+print(sys.argv[1], d["value"], d["ms_per_step"], "frac", (d.get("roofline") or {}).get("frac"), " ".join("%s=%s" % (k, v["ms_per_step"]) for k,v in st.items()))' "$e"
   done
 done

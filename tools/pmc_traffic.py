@@ -20,7 +20,7 @@ def short_name(full: str) -> str:
     if m:  # mangled, non-template: _ZN3sfm12k_match_mfmaE...
         return m.group(2)[: int(m.group(1))]
     name = full.split("(")[0].replace("void ", "").replace("sfm::", "").replace(" ", "")
-    t = re.match(r"(k_harris)<(\d+),(?:true,|false,)?0>", name)
+    t = re.match(r"(k_harris)<(\d+),(?:true,|false,)?0(?:,\d+)?>", name)
     if t:  # both load variants of one window size
         return f"{t.group(1)}<{t.group(2)}>"
     if name.startswith("dq::k_describe_q<"):  # every level's instance
