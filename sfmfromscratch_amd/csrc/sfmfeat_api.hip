@@ -381,9 +381,16 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
         launch_nms(e.R, e.med, e.cand, candcnt + e.co, B, lv[l].h, lv[l].w, c->p.ksize, 0, st);
       }
       if (l < L_aux) {
+        // SFMFEAT_SELECT_CALLER=1 (A/B): the level's selection on the caller's stream ahead of
+        // the next level's Harris, only its descriptors on aux
+        static const bool sel_caller = [] {
+          const char* e = getenv("SFMFEAT_SELECT_CALLER");
+          return e && atoi(e) == 1;
+        }();
+        if (sel_caller) select_level(l, st);
         HIPCHK(c, hipEventRecord(c->ev[l], st));
         HIPCHK(c, hipStreamWaitEvent(ax, c->ev[l], 0));
-        select_level(l, ax);
+        if (!sel_caller) select_level(l, ax);
         if (l == L_aux - 1) HIPCHK(c, hipEventRecord(c->ev[L + 2], ax));  // counts of the aux levels known
         describe_level(l, ax);
       }
