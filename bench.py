@@ -211,7 +211,8 @@ def main():
     dev = torch.device("cuda", local % ngpu)
     if world > 1:
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            from sfmfromscratch_amd.distributed import nccl_options
+            dist.init_process_group("nccl", device_id=dev, pg_options=nccl_options(dist))
         else:
             dist.init_process_group(backend)
 

@@ -21,9 +21,22 @@ from __future__ import annotations
 
 import heapq
 
+import os
+
 import numpy as np
 
 from .pipeline import all_pairs, consecutive_pairs
+
+
+def nccl_options(dist):
+    """Process-group options for the RCCL group of the exchange: its internal stream at high
+    priority (SFM_NCCL_HIPRIO=0 turns it off).  The gather's kernels are a few persistent
+    workgroups per chunk; at the default priority they queue behind the persistent Harris
+    workgroups of the next chunk (both lanes' kernels fill every CU), which would push the
+    gather — and the matching that waits for it — past the extraction it should overlap."""
+    opts = dist.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = os.environ.get("SFM_NCCL_HIPRIO", "1") != "0"
+    return opts
 
 
 def shard_range(n_global: int, world: int, rank: int) -> tuple[int, int]:
