@@ -195,3 +195,14 @@ def test_local_pairs_edge_cases():
     assert D.local_consecutive_pairs(3, 0, 1).tolist() == [[0, 1], [1, 2]]
     a = np.concatenate([D.all_pairs_for_rank(9, r, 4) for r in range(4)])
     assert len(a) == 36 and len({tuple(p) for p in a.tolist()}) == 36
+
+
+def test_nccl_options_high_priority_stream(monkeypatch):
+    """The exchange's RCCL group runs on a high-priority stream unless SFM_NCCL_HIPRIO=0."""
+    import torch.distributed as dist
+
+    from sfmfromscratch_amd.distributed import nccl_options
+    monkeypatch.delenv("SFM_NCCL_HIPRIO", raising=False)
+    assert nccl_options(dist).is_high_priority_stream
+    monkeypatch.setenv("SFM_NCCL_HIPRIO", "0")
+    assert not nccl_options(dist).is_high_priority_stream
