@@ -30,7 +30,10 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(std::make_integer_sequence<int, N>{}, f);
 }
 
-constexpr int kHT = 64;   // output tile: 64 x 64 pixels (16 column groups x 16 row quads)
+constexpr int kHT = 64;   // output tile columns (rows: HarrisShape::TH, 64 or 32)
+// levels with at most this many 64 x 64 tiles per resident workgroup take the 64 x 32 form
+// (SFMFEAT_HARRIS_SMALL overrides; 0 = never)
+constexpr int kHarrisSmallTiles = 0;
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -68,15 +71,27 @@ __device__ uint64_t* g_harris_stamps;
 // SIMD at up to 256 VGPRs.  1: 512 threads x (4 columns x 2 rows), 4 waves per SIMD at up to
 // 128 VGPRs (the window's packed fmas issue faster at 4 waves per SIMD), at
 // the price of each gradient row's products being formed by twice as many threads.
-template <int NPAIR>
+// F (the workgroup form):
+//   0: 256 threads x (4 columns x 4 rows), 64 x 64 tiles, 2 workgroups per CU (2 waves per
+//      SIMD at up to 256 VGPRs) — the default;
+//   1: 512 threads x (4 x 2), 64 x 64 tiles, 2 per CU (4 waves per SIMD at 128 VGPRs);
+//   2: 256 threads x (4 x 2), 64 x 32 tiles, 3 per CU (3 waves per SIMD at 168 VGPRs): the
+//      small levels, whose 64 x 64 tiles would give each resident workgroup only a few
+//      tiles to walk one after another.
+template <int F>
 struct HarrisShape {
-  static constexpr int NT = 512 / NPAIR;   // threads per workgroup (2 workgroups per CU: NT / 128 waves per SIMD)
-  static constexpr int RPT = 2 * NPAIR;    // output rows per thread
+  static constexpr int NPAIR = F == 0 ? 2 : 1;           // output row pairs per thread
+  static constexpr int NT = F == 1 ? 512 : 256;          // threads per workgroup
+  static constexpr int RPT = 2 * NPAIR;                  // output rows per thread
+  static constexpr int TH = RPT * 4 * (NT / 64);         // tile rows (tile columns: kHT)
+  static constexpr int WPC = F == 2 ? 3 : 2;             // workgroups per CU
+  static constexpr int WPE = WPC * NT / 256;             // waves per SIMD
 };
 
-template <int KS, bool VEC, int ABL = 0, int NPAIR = 2>
-__global__ void __launch_bounds__(HarrisShape<NPAIR>::NT, HarrisShape<NPAIR>::NT / 128) k_harris(HarrisLevels lvs, const float* __restrict__ gk, float alpha) {
-  constexpr int NT = HarrisShape<NPAIR>::NT, RPT = HarrisShape<NPAIR>::RPT;
+template <int KS, bool VEC, int ABL = 0, int F = 0>
+__global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_harris(HarrisLevels lvs, const float* __restrict__ gk, float alpha) {
+  constexpr int NT = HarrisShape<F>::NT, RPT = HarrisShape<F>::RPT, NPAIR = HarrisShape<F>::NPAIR;
+  constexpr int TH = HarrisShape<F>::TH;
   // this workgroup's level (one launch may hold several pyramid levels: the small levels'
   // tiles share a launch instead of each paying a launch and a tail)
   int li = 0;
@@ -89,7 +104,7 @@ __global__ void __launch_bounds__(HarrisShape<NPAIR>::NT, HarrisShape<NPAIR>::NT
   const SelectScan scan = lvs.l[li].scan;
   const int wgx = (int)blockIdx.x - lvs.l[li].wg0, nwg = lvs.l[li].nwg;  // workgroups of this level's plane
   constexpr int GA = KS / 2;
-  constexpr int PH = kHT + KS - 1;          // gradient rows of a tile (window halo)
+  constexpr int PH = TH + KS - 1;           // gradient rows of a tile (window halo)
   constexpr int NV = 4 + KS - 1;            // gradient values per row per thread
   constexpr int NV4 = (NV + 3) / 4;         // b128 LDS loads per row per plane
   constexpr int NVP = 4 * NV4;
@@ -147,7 +162,7 @@ __global__ void __launch_bounds__(HarrisShape<NPAIR>::NT, HarrisShape<NPAIR>::NT
   uint64_t okmask = 0;
   auto prefetch = [&](int tile) {
     const int gx0 = (tile % tiles_x) * kHT - XA;
-    const int gy0 = (tile / tiles_x) * kHT - GA - 1;
+    const int gy0 = (tile / tiles_x) * TH - GA - 1;
     okmask = 0;
     if constexpr (VEC) {
 #pragma unroll
@@ -184,7 +199,7 @@ __global__ void __launch_bounds__(HarrisShape<NPAIR>::NT, HarrisShape<NPAIR>::NT
       else __builtin_amdgcn_s_setprio(0);
     }
     const int tx0 = (tile % tiles_x) * kHT;
-    const int ty0 = (tile / tiles_x) * kHT;
+    const int ty0 = (tile / tiles_x) * TH;
     __syncthreads();  // the previous tile's LDS reads are done
     // 0. the prefetched image tile -> LDS, then start fetching the next tile
 #pragma unroll
@@ -426,13 +441,9 @@ __global__ void __launch_bounds__(HarrisShape<NPAIR>::NT, HarrisShape<NPAIR>::NT
 
 // Workgroups per plane for a group of levels: a common tile budget per workgroup
 // T = ceil(sum of tiles / slots per plane), each level gets ceil(tiles / T) workgroups, so
-// every workgroup walks at most T tiles (2 resident per CU over the batch; each loops
-// over tiles so the digit histogram is flushed once per workgroup instead of once per tile)
-static int harris_plan(HarrisLevels& g, int B) {
-  static const int slots = [] {  // SFMFEAT_HARRIS_SLOTS: resident-workgroup budget (A/B timing)
-    const char* e = getenv("SFMFEAT_HARRIS_SLOTS");
-    return e ? std::max(1, atoi(e)) : 512;
-  }();
+// every workgroup walks at most T tiles (`slots` resident over the batch; each loops over
+// tiles so the digit histogram is flushed once per workgroup instead of once per tile)
+static int harris_plan(HarrisLevels& g, int B, int slots) {
   const int per_plane = std::max(1, slots / std::max(B, 1));
   int total = 0;
   for (int k = 0; k < g.n; ++k) total += g.l[k].ntiles;
@@ -446,42 +457,49 @@ static int harris_plan(HarrisLevels& g, int B) {
   return wg;
 }
 
-// SFMFEAT_HARRIS_NPAIR=1|2: output row pairs per thread (A/B timing; see HarrisShape)
-static int harris_npair() {
-  static const int v = [] {
-    const char* e = getenv("SFMFEAT_HARRIS_NPAIR");
-    return (e && atoi(e) == 1) ? 1 : 2;
-  }();
-  return v;
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+
+template <int KS, int ABL, int F>
+static void launch_form(HarrisLevels g, int B, const float* gk, float alpha, hipStream_t st) {
+  using S = HarrisShape<F>;
+  // SFMFEAT_HARRIS_SLOTS: resident-workgroup budget of the default form (A/B timing)
+  static const int slots2 = std::max(1, env_int("SFMFEAT_HARRIS_SLOTS", 512));
+  bool vec = true;
+  for (int k = 0; k < g.n; ++k) {
+    g.l[k].tiles_x = (g.l[k].W + kHT - 1) / kHT;
+    g.l[k].ntiles = g.l[k].tiles_x * ((g.l[k].H + S::TH - 1) / S::TH);
+    vec = vec && (g.l[k].W & 3) == 0;
+  }
+  const int nwg = harris_plan(g, B, slots2 * S::WPC / 2);
+  if (vec)
+    hipLaunchKernelGGL((k_harris<KS, true, ABL, F>), dim3(nwg, B), dim3(S::NT), 0, st, g, gk, alpha);
+  else
+    hipLaunchKernelGGL((k_harris<KS, false, ABL, F>), dim3(nwg, B), dim3(S::NT), 0, st, g, gk, alpha);
 }
 
 template <int KS, int ABL = 0>
 static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipStream_t st) {
-  static const int prio = [] {  // SFMFEAT_HARRIS_PRIO=1: tile-balancing issue priority (A/B)
-    const char* e = getenv("SFMFEAT_HARRIS_PRIO");
-    return e ? atoi(e) : 0;
-  }();
+  // SFMFEAT_HARRIS_PRIO=1: tile-balancing issue priority (A/B)
+  static const int prio = env_int("SFMFEAT_HARRIS_PRIO", 0);
+  // SFMFEAT_HARRIS_NPAIR=1: the four-wave form for every level (A/B)
+  static const int npair = env_int("SFMFEAT_HARRIS_NPAIR", 2);
+  // SFMFEAT_HARRIS_SMALL=t: levels whose 64 x 64 tiles number at most t per resident
+  // workgroup (over the batch) take the 64 x 32 form (0: never)
+  static const int small = env_int("SFMFEAT_HARRIS_SMALL", kHarrisSmallTiles);
   g.prio = prio;
-  bool vec = true;
-  for (int k = 0; k < g.n; ++k) {
-    g.l[k].tiles_x = (g.l[k].W + kHT - 1) / kHT;
-    g.l[k].ntiles = g.l[k].tiles_x * ((g.l[k].H + kHT - 1) / kHT);
-    vec = vec && (g.l[k].W & 3) == 0;
+  if constexpr (KS == 7) {  // the alternative forms are built for the 7 x 7 window only
+    if (npair == 1) return launch_form<KS, ABL, 1>(g, B, gk, alpha, st);
+    bool sm = small > 0;
+    for (int k = 0; k < g.n; ++k) {
+      const int64_t t64 = (int64_t)((g.l[k].W + kHT - 1) / kHT) * ((g.l[k].H + kHT - 1) / kHT) * B;
+      sm = sm && t64 <= (int64_t)small * 512;
+    }
+    if (sm) return launch_form<KS, ABL, 2>(g, B, gk, alpha, st);
   }
-  const int nwg = harris_plan(g, B);
-  if (harris_npair() == 1) {
-    constexpr int NT = HarrisShape<1>::NT;
-    if (vec)
-      hipLaunchKernelGGL((k_harris<KS, true, ABL, 1>), dim3(nwg, B), dim3(NT), 0, st, g, gk, alpha);
-    else
-      hipLaunchKernelGGL((k_harris<KS, false, ABL, 1>), dim3(nwg, B), dim3(NT), 0, st, g, gk, alpha);
-  } else {
-    constexpr int NT = HarrisShape<2>::NT;
-    if (vec)
-      hipLaunchKernelGGL((k_harris<KS, true, ABL, 2>), dim3(nwg, B), dim3(NT), 0, st, g, gk, alpha);
-    else
-      hipLaunchKernelGGL((k_harris<KS, false, ABL, 2>), dim3(nwg, B), dim3(NT), 0, st, g, gk, alpha);
-  }
+  launch_form<KS, ABL, 0>(g, B, gk, alpha, st);
 }
 
 void launch_harris_levels(const HarrisLevels& g, int B, const float* d_gauss, int ks, float alpha, hipStream_t st) {
