@@ -34,6 +34,8 @@ constexpr int kHT = 64;   // output tile columns (rows: HarrisShape::TH, 64 or 3
 // levels with at most this many 64 x 64 tiles per resident workgroup take the 64 x 32 form
 // (SFMFEAT_HARRIS_SMALL overrides; 0 = never)
 constexpr int kHarrisSmallTiles = 0;
+// 1: the 7 x 7 window's default form keeps product planes in LDS (form 3; SFMFEAT_HARRIS_PP)
+constexpr int kHarrisProductPlanes = 0;
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -77,10 +79,15 @@ __device__ uint64_t* g_harris_stamps;
 //   1: 512 threads x (4 x 2), 64 x 64 tiles, 2 per CU (4 waves per SIMD at 128 VGPRs);
 //   2: 256 threads x (4 x 2), 64 x 32 tiles, 3 per CU (3 waves per SIMD at 168 VGPRs): the
 //      small levels, whose 64 x 64 tiles would give each resident workgroup only a few
-//      tiles to walk one after another.
+//      tiles to walk one after another;
+//   3: as 0, but the Sobel phase forms the three products once per pixel and LDS holds
+//      product planes Ix^2, Iy^2, IxIy (the image tile aliased into them) instead of the two
+//      gradient planes, so the window phase reads products instead of re-forming them for
+//      every row it feeds (each gradient row's products were formed by 2.5 threads).
 template <int F>
 struct HarrisShape {
-  static constexpr int NPAIR = F == 0 ? 2 : 1;           // output row pairs per thread
+  static constexpr bool PP = F == 3;                     // product planes in LDS
+  static constexpr int NPAIR = (F == 0 || F == 3) ? 2 : 1;  // output row pairs per thread
   static constexpr int NT = F == 1 ? 512 : 256;          // threads per workgroup
   static constexpr int RPT = 2 * NPAIR;                  // output rows per thread
   static constexpr int TH = RPT * 4 * (NT / 64);         // tile rows (tile columns: kHT)
@@ -92,6 +99,7 @@ template <int KS, bool VEC, int ABL = 0, int F = 0>
 __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_harris(HarrisLevels lvs, const float* __restrict__ gk, float alpha) {
   constexpr int NT = HarrisShape<F>::NT, RPT = HarrisShape<F>::RPT, NPAIR = HarrisShape<F>::NPAIR;
   constexpr int TH = HarrisShape<F>::TH;
+  constexpr bool PP = HarrisShape<F>::PP;
   // this workgroup's level (one launch may hold several pyramid levels: the small levels'
   // tiles share a launch instead of each paying a launch and a tail)
   int li = 0;
@@ -124,8 +132,13 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   constexpr int IW4 = IWP / 4;
   constexpr int NIMG = VEC ? (IH * IW4 + NT - 1) / NT : (IH * IWP + NT - 1) / NT;
   static_assert(NIMG <= 64, "prefetch mask");
-  __shared__ __attribute__((aligned(16))) float s_g[2][PH][PWP];
-  __shared__ __attribute__((aligned(16))) float s_img[IH][IWP];
+  // gradient planes (or, PP, product planes) and the image tile; PP aliases the image tile
+  // into the product planes (the tile is dead once the Sobel pass has read it)
+  constexpr int NPL = PP ? 3 : 2;
+  static_assert(!PP || IH * IWP <= NPL * PH * PWP, "image tile alias");
+  __shared__ __attribute__((aligned(16))) float s_pl[NPL * PH * PWP + (PP ? 0 : IH * IWP)];
+  float (*const s_g)[PH][PWP] = reinterpret_cast<float (*)[PH][PWP]>(s_pl);
+  float (*const s_img)[IWP] = reinterpret_cast<float (*)[IWP]>(s_pl + (PP ? 0 : NPL * PH * PWP));
   __shared__ uint32_t s_hist[kMedBins1];  // digit-1 histogram, flushed once per workgroup
   // tap pairs per gradient row r and row pair p: (g[r-2p][j], g[r-2p-1][j]), 0 where the
   // tap row does not exist; read as uniform LDS broadcasts (49 taps in SGPRs spill)
@@ -215,16 +228,22 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
       }
     }
     __syncthreads();
-    if (tile + nwg < ntiles) prefetch(tile + nwg);
+    // (PP: after the product pass, so the prefetch registers are not live beside the
+    // strips' gradients)
+    if (!PP && tile + nwg < ntiles) prefetch(tile + nwg);
     // 1. gradients (NaiveSIFT.py:201-213: fma chain over the non-zero Sobel taps in
     //    row-major order from +0; k*p is exact for these taps) for 4-wide strips; outside
     //    the image the gradients are 0, so their products (:61-63) are the zero border of
     //    the window sums (:67-69)
     //    Packed over column pairs (q, q+1) when the strip's image reads are pair-aligned
     //    (each half an IEEE fma, as the scalar chain); interior tiles skip the masking.
+    constexpr int NSI = (PH * NS + NT - 1) / NT;  // strips per thread (PP: held in registers)
+    float4 GXs[PP ? NSI : 1], GYs[PP ? NSI : 1];
     auto sobel = [&](auto maskedc) {
       constexpr bool MASKED = decltype(maskedc)::value;
-      for (int sidx = tid; sidx < PH * NS; sidx += NT) {
+#pragma unroll
+      for (int it = 0; it < (PP ? NSI : 1); ++it)
+      for (int sidx = tid + it * NT; sidx < PH * NS; sidx += (PP ? PH * NS : NT)) {
         const int py = sidx / NS, px0 = (sidx - py * NS) * 4;
         f32x2 w[3][2 * NR4];
 #pragma unroll
@@ -299,8 +318,13 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
             gyq[q] = inside ? gyq[q] : 0.0f;
           }
         }
-        *reinterpret_cast<float4*>(&s_g[0][py][px0]) = make_float4(gxq[0], gxq[1], gxq[2], gxq[3]);
-        *reinterpret_cast<float4*>(&s_g[1][py][px0]) = make_float4(gyq[0], gyq[1], gyq[2], gyq[3]);
+        if constexpr (PP) {
+          GXs[it] = make_float4(gxq[0], gxq[1], gxq[2], gxq[3]);
+          GYs[it] = make_float4(gyq[0], gyq[1], gyq[2], gyq[3]);
+        } else {
+          *reinterpret_cast<float4*>(&s_g[0][py][px0]) = make_float4(gxq[0], gxq[1], gxq[2], gxq[3]);
+          *reinterpret_cast<float4*>(&s_g[1][py][px0]) = make_float4(gyq[0], gyq[1], gyq[2], gyq[3]);
+        }
       }
     };
     // every gradient position of the tile (incl. the unused stride padding) in the image
@@ -308,6 +332,25 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     if (grad_in) sobel(std::false_type{});
     else sobel(std::true_type{});
     __syncthreads();
+    if constexpr (PP) {
+      // the image tile is dead: the three products of every gradient (NaiveSIFT.py:61-63, the
+      // same IEEE products the window phase formed) into their planes
+#pragma unroll
+      for (int it = 0; it < NSI; ++it) {
+        const int sidx = tid + it * NT;
+        if (sidx < PH * NS) {
+          const int py = sidx / NS, px0 = (sidx - py * NS) * 4;
+          const f32x2 x0 = {GXs[it].x, GXs[it].y}, x1 = {GXs[it].z, GXs[it].w};
+          const f32x2 y0 = {GYs[it].x, GYs[it].y}, y1 = {GYs[it].z, GYs[it].w};
+          const f32x2 a0 = x0 * x0, a1 = x1 * x1, b0 = y0 * y0, b1 = y1 * y1, c0 = x0 * y0, c1 = x1 * y1;
+          *reinterpret_cast<float4*>(&s_g[0][py][px0]) = make_float4(a0.x, a0.y, a1.x, a1.y);
+          *reinterpret_cast<float4*>(&s_g[1][py][px0]) = make_float4(b0.x, b0.y, b1.x, b1.y);
+          *reinterpret_cast<float4*>(&s_g[2][py][px0]) = make_float4(c0.x, c0.y, c1.x, c1.y);
+        }
+      }
+      __syncthreads();
+      if (tile + nwg < ntiles) prefetch(tile + nwg);
+    }
 
     // 2. window sums (:67-69): per pixel an fma chain over the KS x KS taps in row-major
     //    order.  acc[p][pl][q] = (row 4rq+2p, row 4rq+2p+1) at column 4tq+q; gradient row
@@ -324,7 +367,18 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     static_for<NR>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
       f32x2 P[3][NP2];
-      {
+      if constexpr (PP) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          const float4* rp = reinterpret_cast<const float4*>(&s_g[pl][RPT * rq + r][4 * tq]);
+#pragma unroll
+          for (int c4 = 0; c4 < NV4; ++c4) {
+            const float4 a = rp[c4];
+            if (2 * c4 < NP2) P[pl][2 * c4] = f32x2{a.x, a.y};
+            if (2 * c4 + 1 < NP2) P[pl][2 * c4 + 1] = f32x2{a.z, a.w};
+          }
+        }
+      } else {
         const float4* rx = reinterpret_cast<const float4*>(&s_g[0][RPT * rq + r][4 * tq]);
         const float4* ry = reinterpret_cast<const float4*>(&s_g[1][RPT * rq + r][4 * tq]);
         f32x2 X[NVP / 2], Y[NVP / 2];
@@ -490,6 +544,8 @@ static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipSt
   // workgroup (over the batch) take the 64 x 32 form (0: never)
   static const int small = env_int("SFMFEAT_HARRIS_SMALL", kHarrisSmallTiles);
   g.prio = prio;
+  // SFMFEAT_HARRIS_PP=1: product planes in LDS (form 3) instead of gradient planes (A/B)
+  static const int pp = env_int("SFMFEAT_HARRIS_PP", kHarrisProductPlanes);
   if constexpr (KS == 7) {  // the alternative forms are built for the 7 x 7 window only
     if (npair == 1) return launch_form<KS, ABL, 1>(g, B, gk, alpha, st);
     bool sm = small > 0;
@@ -498,6 +554,7 @@ static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipSt
       sm = sm && t64 <= (int64_t)small * 512;
     }
     if (sm) return launch_form<KS, ABL, 2>(g, B, gk, alpha, st);
+    if (pp == 1) return launch_form<KS, ABL, 3>(g, B, gk, alpha, st);
   }
   launch_form<KS, ABL, 0>(g, B, gk, alpha, st);
 }
