@@ -519,8 +519,13 @@ static int env_int(const char* name, int dflt) {
 template <int KS, int ABL, int F>
 static void launch_form(HarrisLevels g, int B, const float* gk, float alpha, hipStream_t st) {
   using S = HarrisShape<F>;
-  // SFMFEAT_HARRIS_SLOTS: resident-workgroup budget of the default form (A/B timing)
-  static const int slots2 = std::max(1, env_int("SFMFEAT_HARRIS_SLOTS", 512));
+  // Resident-workgroup budget of the default form (SFMFEAT_HARRIS_SLOTS overrides).  Batches
+  // of >= 16 planes take 448 = 14 workgroups per plane at 32 planes, which leaves 64 CUs
+  // with one Harris workgroup instead of two for the other batch in flight: measured 33.4k
+  // -> 34.8-35.5k img/s on the headline (13 per plane: 33.0k, 15: 32.5k, 16: 33.4k, 18:
+  // 34.2-34.6k); at 8 planes of 4K it cost 6 %, so small batches keep 512.
+  static const int slots_env = env_int("SFMFEAT_HARRIS_SLOTS", 0);
+  const int slots2 = slots_env > 0 ? slots_env : (B >= 16 ? 448 : 512);
   bool vec = true;
   for (int k = 0; k < g.n; ++k) {
     g.l[k].tiles_x = (g.l[k].W + kHT - 1) / kHT;
