@@ -33,7 +33,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 constexpr int kHT = 64;   // output tile columns (rows: HarrisShape::TH, 64 or 32)
 // levels with at most this many 64 x 64 tiles per resident workgroup take the 64 x 32 form
 // (SFMFEAT_HARRIS_SMALL overrides; 0 = never)
-constexpr int kHarrisSmallTiles = 0;
+constexpr int kHarrisSmallTiles = 4;
 // 1: the 7 x 7 window's default form keeps product planes in LDS (form 3; SFMFEAT_HARRIS_PP)
 constexpr int kHarrisProductPlanes = 0;
 
