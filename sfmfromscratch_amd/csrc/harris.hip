@@ -523,12 +523,13 @@ static void launch_form(HarrisLevels g, int B, const float* gk, float alpha, hip
   // of >= 16 planes take 448 = 14 workgroups per plane at 32 planes, which leaves 64 CUs
   // with one Harris workgroup instead of two for the other batch in flight: measured 33.4k
   // -> 34.8-35.5k img/s on the headline (13 per plane: 33.0k, 15: 32.5k, 16: 33.4k, 18:
-  // 34.2-34.6k); at 8 planes of 4K it cost 6 %, so small batches keep 512.
+  // 34.2-34.6k); at 8 planes of 4K 448 cost 6 % and 480 (60 per plane)
+  // measured best (6.15-6.17k against 5.98-6.00k img/s at 512, 5.95k at 576, 5.87k at 640).
   static const int slots_env = env_int("SFMFEAT_HARRIS_SLOTS", 0);
   // SFMFEAT_HARRIS_SLOTS_UPPER=n (A/B): the budget of levels above the first (fewer than
   // 200 64 x 64 tiles per plane)
   static const int slots_up = env_int("SFMFEAT_HARRIS_SLOTS_UPPER", 0);
-  int slots2 = slots_env > 0 ? slots_env : (B >= 16 ? 448 : 512);
+  int slots2 = slots_env > 0 ? slots_env : (B >= 16 ? 448 : 480);
   if (slots_up > 0 && g.n == 1 && ((g.l[0].W + kHT - 1) / kHT) * ((g.l[0].H + kHT - 1) / kHT) < 200) slots2 = slots_up;
   bool vec = true;
   for (int k = 0; k < g.n; ++k) {
