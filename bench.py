@@ -159,6 +159,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=8,
                     help="frames per host thread in the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-profile", action="store_true", help="disable the live per-stage HIP events")
+    ap.add_argument("--events-in-timed", action="store_true",
+                    help="A/B: bracket the dominant stage's launches with HIP events inside the timed region "
+                         "(default: a second, separate run of the same steps carries them)")
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default=None,
                     help="default: c2 at one GPU, c4 at N > 1.  "
                          "c2 = BASELINE configs[1] (the headline line); c3 = configs[2] (256 frames, all "
@@ -268,11 +271,6 @@ def main():
         def step():
             pipe.submit(frames, hook=halo)
 
-    for _ in range(args.warmup):
-        step()
-    pipe.join()
-    torch.cuda.synchronize()
-
     def stage_work(counts, nsteps):
         """Algorithmic work of `nsteps` steps per stage:
         (bound, amount, unit, peak, algorithmic HBM bytes or None).  Latency-bound stages
@@ -363,20 +361,37 @@ def main():
                       "keypoints_per_level": [int(v) for v in lvl_kp],
                       "note": "modelled lane-ops per keypoint (bench.describe_ops) / 39.3 T lane-op/s"})
         dom = max((k for k in prof_all if k in work and prof_all[k][1]), key=lambda k: prof_all[k][0])
-        for c in ctxs:
-            c.profile_stages([dom])
+        prof_enable(False)
         prof_read()
+
+    def run_steps(nsteps, step_events=None):
+        """nsteps steps of the two-lane pipeline from an idle GPU; with step_events, one
+        timing event per step on its lane's stream right after its match (the step's end)."""
+        pipe.start()
+        for _ in range(nsteps):
+            step()
+            if step_events is not None:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(pipe.lanes[(pipe.n - 1) % pipe.inflight]["stream"])
+                step_events.append(e)
+        pipe.join()
+
+    # W warm-up steps: the same two-lane pipeline as the timed steps, right before them
+    run_steps(args.warmup)
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    step_ev = []
+    if dom and args.events_in_timed:  # A/B: the per-launch events inside the timed region
+        for c in ctxs:
+            c.profile_stages([dom])
     t0 = time.perf_counter()
     ev0.record()
-    pipe.start()
-    for _ in range(args.steps):
-        step()
-    pipe.join()
+    run_steps(args.steps, step_ev)
+    t_sub = time.perf_counter() - t0
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -388,9 +403,30 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    # per-step end times inside the timed region (not part of `value`)
+    step_end = [ev0.elapsed_time(e) for e in step_ev]
+    step_detail = {"end_ms": [round(x, 4) for x in step_end],
+                   "first_step_ms": round(step_end[0], 4) if step_end else None,
+                   "steady_ms_per_step": (round((step_end[-1] - step_end[len(step_end) // 2]) /
+                                                max(1, len(step_end) - 1 - len(step_end) // 2), 4)
+                                          if len(step_end) > 2 else None),
+                   "host_submit_ms": round(t_sub * 1e3, 3)}
 
-    prof = prof_read() if dom else {}
-    prof_enable(False)
+    # the roofline: the same two-lane pipeline again, K steps, with HIP events around each
+    # launch of the dominant stage (kept out of the timed region above)
+    prof = {}
+    if dom and args.events_in_timed:
+        prof = prof_read()
+        prof_enable(False)
+    elif dom:
+        for c in ctxs:
+            c.profile_stages([dom])
+        prof_read()
+        torch.cuda.synchronize()
+        run_steps(args.steps)
+        torch.cuda.synchronize()
+        prof = prof_read()
+        prof_enable(False)
     counts = lane_counts()
     nmatch = pipe.lanes[0]["mout"][2].cpu().numpy()
 
@@ -415,8 +451,11 @@ def main():
                 "algorithmic_bytes_per_launch": round(alg_per_launch) if alg_per_launch else None,
                 "traffic_ratio": round(tr / alg_per_launch, 3) if tr and alg_per_launch else None,
                 "avg_launch_ms": round(ms / max(n, 1), 4), "launches": n,
-                "timing": "HIP events around each launch of the stage inside the timed region "
-                          f"({args.inflight} batches in flight)"}
+                "timing": (f"HIP events around each launch of the stage inside the timed region "
+                           f"({args.inflight} batches in flight)") if args.events_in_timed else
+                          (f"HIP events around each launch of the stage, on its stream, over a second run of the "
+                           f"timed region's {args.steps} steps ({args.inflight} batches in flight); the timed "
+                           f"region itself runs without per-launch events")}
         if tr is not None:
             roof["traffic_note"] = "HBM bytes per launch, rocprofv3 PMC (profiles/pmc_traffic.json)"
 
@@ -456,6 +495,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "stages_ms": stages,
+            "steps_detail": step_detail,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -632,14 +672,9 @@ def run_gather(args, torch, dist, dev, rank, world):
     verified = None
     if world > 1 and not job.halo:
         bad = job.verify_exchange()
-        if bad and job.coalesce:  # grouped collective misbehaved: fall back to one per field
-            log(f"exchange check: {bad} frames differ with the coalesced gather; using one collective per field")
-            job.coalesce = False
-            job.run(frames, record_sent=True)
-            torch.cuda.synchronize()
-            bad = job.verify_exchange()
-        if bad:
-            raise SystemExit(f"exchange check failed: {bad} of {n_global} gathered frames differ from their owner's")
+        if bad:  # a wrong exchange ends the run: no silent switch to another collective
+            raise SystemExit(f"exchange check failed: {bad} of {n_global} gathered frames differ from their owner's "
+                             f"({'coalesced' if job.coalesce else 'per-field'} all-gather)")
         verified = n_global
 
     comm = None

@@ -157,7 +157,9 @@ float sfm_debug_harris_stamps(int32_t device, int32_t abl, int32_t B, int32_t H,
   (void)hipMemcpy(d_img, h.data(), n * 4, hipMemcpyHostToDevice);
   (void)hipMemcpy(d_g, g, 4 * 49, hipMemcpyHostToDevice);
   (void)hipMemset(d_hist, 0, (size_t)B * 4 * kMedBins1);
-  float ms = time_harris_ablation(abl, d_img, d_R, d_hist, B, H, W, d_g, 0.05f, iters, d_st);
+  // the kernel skips the stamps of workgroups whose slots lie beyond cap (the grid is
+  // chosen inside the launcher, so the caller cannot size cap exactly)
+  float ms = time_harris_ablation(abl, d_img, d_R, d_hist, B, H, W, d_g, 0.05f, iters, d_st, d_st ? cap : 0);
   if (d_st) {
     (void)hipMemcpy(out, d_st, (size_t)cap * 8, hipMemcpyDeviceToHost);
     (void)hipFree(d_st);

@@ -43,6 +43,11 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // fmaf) with the product value broadcast to both halves by op_sel — no register shuffles.
 template <int H>
 __device__ __forceinline__ void pk_fma_bcast(f32x2& acc, f32x2 k, f32x2 v) {
+#ifdef SFM_HARRIS_NATIVE_PK
+  const float b = v[H];
+  acc = __builtin_elementwise_fma(k, f32x2{b, b}, acc);
+  return;
+#endif
   if constexpr (H == 0)
     asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "v"(k), "v"(v));
   else
@@ -68,6 +73,7 @@ __device__ __forceinline__ void pk_fma_bcast(f32x2& acc, f32x2 k, f32x2 v) {
 // each tile ...} (s_memrealtime, 100 MHz)
 constexpr int kStampSlots = 48;
 __device__ uint64_t* g_harris_stamps;
+__device__ int64_t g_harris_stamps_cap;  // u64 slots behind g_harris_stamps (workgroups beyond it skip)
 
 // NPAIR: output row pairs per thread.  2: 256 threads x (4 columns x 4 rows), 2 waves per
 // SIMD at up to 256 VGPRs.  1: 512 threads x (4 columns x 2 rows), 4 waves per SIMD at up to
@@ -150,8 +156,9 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   uint64_t* stamp = nullptr;
   int nst = 0;
   if constexpr (ABL == 3) {
-    stamp = g_harris_stamps + ((int64_t)b * gridDim.x + blockIdx.x) * kStampSlots;
-    if (tid == 0) {
+    const int64_t s0 = ((int64_t)b * gridDim.x + blockIdx.x) * kStampSlots;
+    stamp = s0 + kStampSlots <= g_harris_stamps_cap ? g_harris_stamps + s0 : nullptr;
+    if (tid == 0 && stamp) {
       stamp[0] = wall_clock64();
       stamp[2] = (uint64_t)__smid();
     }
@@ -462,12 +469,12 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
       }
     }
     if constexpr (ABL == 3) {
-      if (tid == 0 && nst < kStampSlots - 4) stamp[4 + nst] = wall_clock64();
+      if (tid == 0 && stamp && nst < kStampSlots - 4) stamp[4 + nst] = wall_clock64();
       ++nst;
     }
   }  // tile loop
   if constexpr (ABL == 3) {
-    if (tid == 0) {
+    if (tid == 0 && stamp) {
       stamp[1] = wall_clock64();
       stamp[3] = (uint64_t)nst;
     }
@@ -612,8 +619,11 @@ void launch_harris(const float* lvl, float* R, uint32_t* hist, int B, int H, int
 
 // Ablation timing (diagnostics): KS = 7 only, returns the mean launch time in ms.
 float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
-                           const float* gk, float alpha, int iters, uint64_t* stamps) {
-  if (abl == 3) (void)hipMemcpyToSymbol(HIP_SYMBOL(g_harris_stamps), &stamps, sizeof(stamps));
+                           const float* gk, float alpha, int iters, uint64_t* stamps, int64_t stamps_cap) {
+  if (abl == 3) {
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_harris_stamps), &stamps, sizeof(stamps));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_harris_stamps_cap), &stamps_cap, sizeof(stamps_cap));
+  }
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);

@@ -216,7 +216,8 @@ void launch_harris_levels(const HarrisLevels& g, int B, const float* d_gauss, in
                           hipStream_t st);
 
 float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
-                           const float* gk, float alpha, int iters, uint64_t* stamps = nullptr);
+                           const float* gk, float alpha, int iters, uint64_t* stamps = nullptr,
+                           int64_t stamps_cap = 0);
 
 // median.hip.  launch_select_scan: median buckets + certified threshold per plane
 // (vmin = pixels required at or above the threshold).  launch_median_exact: the exact

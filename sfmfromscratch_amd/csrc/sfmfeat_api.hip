@@ -223,10 +223,15 @@ int reserve_impl(sfm_ctx* c, int B, int H, int W) {
   if ((rc = ensure(c, c->d_R, (size_t)B * (A0 + Arest) * 4))) return rc;       // one R map per level
   if ((rc = ensure(c, c->d_hist, (size_t)c->L * B * kMedBins1 * 4))) return rc;
   if ((rc = ensure(c, c->d_med, (size_t)c->L * B * sizeof(MedianState)))) return rc;
-  if ((rc = ensure(c, c->d_medlist, (size_t)2 * B * A0 * 4))) return rc;     // aux | main stream
+  // keypoint-selection scratch (tie lists) and exact-median lists: the aux stream's levels
+  // share region [0, B*A0); the caller stream's levels each own a region starting at B*A0,
+  // packed by level (extract_impl); SFMFEAT_SERIAL puts every level's region from 0.
+  // B * (A0 + A0 + Arest) covers both layouts at any pyramid_scale_factor.
+  const size_t sel_slots = (size_t)B * (2 * A0 + Arest);
+  if ((rc = ensure(c, c->d_medlist, sel_slots * 4))) return rc;
   if ((rc = ensure(c, c->d_counts, (size_t)4 * c->L * B * 8 * kCounterStride))) return rc;
   if ((rc = ensure(c, c->d_cand, (size_t)B * (A0 + Arest) * 8))) return rc;    // candidates per level
-  if ((rc = ensure(c, c->d_scratch, (size_t)2 * B * A0 * 8))) return rc;     // aux | main stream
+  if ((rc = ensure(c, c->d_scratch, sel_slots * 8))) return rc;
   size_t nk = (size_t)c->L * B * (size_t)std::max(c->kcap, 1);
   if ((rc = ensure(c, c->d_kpx, nk * 4))) return rc;
   if ((rc = ensure(c, c->d_kpy, nk * 4))) return rc;

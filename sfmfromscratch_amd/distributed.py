@@ -278,11 +278,14 @@ class ChunkedGatherJob:
     `run(frames)` enqueues one whole job on the caller's stream (no host sync, except for
     'all' pairs, whose deal needs the gathered counts).  Results: `table` (the global
     slot table), `sched` (per chunk: the table-slot pairs this rank matched) and `outs`
-    (per chunk: matches, conf, nmatch)."""
+    (per chunk: matches, conf, nmatch).  'all' pairs: `last_all_pairs` (the dealt
+    table-slot pairs) and, with keep_all_results, `out_all` holding every one of their
+    results (P x cap x 12 B); without it `out_all` is one reused 4,096-pair buffer that
+    keeps only the last sub-batch (timing runs)."""
 
     def __init__(self, extractor_params: dict | None, ratio: float, plan: GatherPlan, rank: int, H: int, W: int,
                  dist=None, inflight: int = 2, exchange: str = "allgather", device: int = 0, group=None,
-                 coalesce: bool | None = None):
+                 coalesce: bool | None = None, keep_all_results: bool = False):
         import torch
         from .pipeline import BatchExtractor, BatchMatcher, SlotTable
         self.torch, self.plan, self.rank, self.dist, self.group = torch, plan, rank, dist, group
@@ -326,7 +329,8 @@ class ChunkedGatherJob:
                 self.rank_pairs_n = len(rp)
         for ln in self.lanes:
             ln["slots"] = SlotTable(torch, Bx, cap, dev) if world > 1 and not self.halo else None
-        self.CH = 4096  # 'all': pairs per matcher launch (output buffer reused)
+        self.CH = 4096  # 'all': pairs per matcher launch
+        self.keep_all_results = bool(keep_all_results)
         if self.sched is not None:
             self.sched_dev = [torch.from_numpy(np.ascontiguousarray(p, np.int32)).to(dev) for p in self.sched]
             self.outs = [self._new_out(len(p)) for p in self.sched]
@@ -425,10 +429,14 @@ class ChunkedGatherJob:
             mine = weighted_deal(self.all_pairs, counts[plan.slot_of(np.arange(plan.n))], world)[rank]
             sp = torch.from_numpy(plan.slot_of(mine).reshape(-1, 2)).to(self.dev)
             self.matcher.prep(self.table)
+            if self.keep_all_results and self.out_all[2].shape[0] < len(sp):
+                self.out_all = self._new_out(len(sp))
             out = self.out_all
             for a in range(0, len(sp), self.CH):
                 n = min(self.CH, len(sp) - a)
-                self.matcher.match(self.table, sp[a:a + n], out=(out[0][:n], out[1][:n], out[2][:n]), prepped=True)
+                o = a if self.keep_all_results else 0  # else: the one reused sub-batch buffer
+                self.matcher.match(self.table, sp[a:a + n], out=(out[0][o:o + n], out[1][o:o + n], out[2][o:o + n]),
+                                   prepped=True)
             self.pairs_matched = len(mine)
             self.last_all_pairs = sp
 

@@ -49,8 +49,12 @@ def _check_job_vs_oracle(torch, job):
         assert np.array_equal(desc[t, :n].view(np.uint32), OD.view(np.uint32)), g
         od[t] = OD
     checked = 0
-    for c, sp in enumerate(job.sched):
-        mm, mc, nm = (o.cpu().numpy() for o in job.outs[c])
+    if job.sched is None:  # 'all' pairs: the dealt pairs and their kept results
+        groups = [(job.last_all_pairs.cpu().numpy(), job.out_all)]
+    else:
+        groups = list(zip(job.sched, job.outs))
+    for sp, outs in groups:
+        mm, mc, nm = (o.cpu().numpy() for o in outs)
         for k, (a, b) in enumerate(np.asarray(sp).tolist()):
             om, oc = O.match(od[a], od[b], RATIO)
             kk = int(nm[k])
@@ -76,6 +80,19 @@ def test_chunked_gather_job_world1_vs_oracle(pairs):
     job.run(frames)  # a second job on the same buffers (lanes / prepped operands reused)
     checked = _check_job_vs_oracle(torch, job)
     assert checked == len(plan.global_pairs())
+
+
+def test_chunked_gather_job_all_pairs_keeps_every_result():
+    """'all' pairs with keep_all_results: 10 frames (45 pairs, more than one 4,096-pair
+    sub-batch would need at CH = 16) keep every pair's result, each equal to O.match."""
+    torch = pytest.importorskip("torch")
+    from sfmfromscratch_amd import distributed as D
+    plan = D.GatherPlan(10, 1, 4, "all")
+    job = D.ChunkedGatherJob(PP, RATIO, plan, 0, H, W, inflight=2, keep_all_results=True)
+    job.CH = 16  # several sub-batches
+    frames = _frames(torch, plan, 0)
+    job.run(frames)
+    assert _check_job_vs_oracle(torch, job) == 45
 
 
 def _free_port() -> int:

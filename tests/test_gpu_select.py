@@ -34,18 +34,22 @@ def mixed_batch(H, W):
     return np.stack([textured, blobs, const, noise])
 
 
-def run(imgs, pp, exact):
+def run(imgs, pp, exact, serial=False):
     import torch
     from sfmfromscratch_amd.pipeline import BatchExtractor
-    old = os.environ.pop("SFMFEAT_SELECT", None)
+    # both switches are read when the context is created
+    old = {k: os.environ.pop(k, None) for k in ("SFMFEAT_SELECT", "SFMFEAT_SERIAL")}
     try:
         if exact:
             os.environ["SFMFEAT_SELECT"] = "exact"
+        if serial:
+            os.environ["SFMFEAT_SERIAL"] = "1"
         ex = BatchExtractor(pp)
     finally:
-        os.environ.pop("SFMFEAT_SELECT", None)
-        if old is not None:
-            os.environ["SFMFEAT_SELECT"] = old
+        for k, v in old.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
     s = ex.extract(torch.from_numpy(imgs).cuda())
     torch.cuda.synchronize()
     stats = ex.ctx.select_stats()
@@ -89,3 +93,24 @@ def test_1080p_planes_certify():
         n = cnt[b]
         assert np.array_equal(xy[b, :n], xe[b, :n])
         assert np.array_equal(bits(desc[b, :n]), bits(de[b, :n]))
+
+
+@pytest.mark.parametrize("exact,serial", [(False, False), (True, False), (True, True)])
+def test_scale_1_1_four_levels_selection_regions_vs_oracle(exact, serial):
+    """pyramid_scale_factor 1.1 (the reference's main.py:19-28 parameters) keeps every level large, so the caller stream's merged selection
+    regions (one per level, packed after the aux stream's) and the serial layout (every
+    level from 0) cover far more than 2 x B x A0 slots.  Noise planes give C > 2048
+    candidates, so the tie lists are written; the exact path writes the median lists.
+    Every plane must still equal the oracle (sfmfeat_api.hip reserve_impl sizes both)."""
+    pp = dict(P_MAIN, num_interest_points=2000, pyramid_level=4, pyramid_scale_factor=1.1)
+    H, W = 360, 640
+    rng = np.random.default_rng(11)
+    imgs = np.stack([synth.make_frame(H, W, 1234, 0), (rng.integers(0, 256, (H, W)) / 255.0).astype(np.float32),
+                     synth.make_frame(H, W, 1234, 1), (rng.integers(0, 256, (H, W)) / 255.0).astype(np.float32)])
+    xy, desc, cnt, _ = run(imgs, pp, exact=exact, serial=serial)
+    for b in range(len(imgs)):
+        n = cnt[b]
+        X, Y, D, _ = O.extract(imgs[b], pp)
+        assert n == len(X)
+        assert np.array_equal(xy[b, :n, 0], X) and np.array_equal(xy[b, :n, 1], Y)
+        assert np.array_equal(bits(desc[b, :n]), bits(D))
