@@ -43,9 +43,13 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // fmaf) with the product value broadcast to both halves by op_sel — no register shuffles.
 template <int H>
 __device__ __forceinline__ void pk_fma_bcast(f32x2& acc, f32x2 k, f32x2 v) {
-#ifdef SFM_HARRIS_NATIVE_PK
+#if defined(SFM_HARRIS_NATIVE_PK)  // diagnostics builds only (tools/coresidency_repro.hip)
   const float b = v[H];
   acc = __builtin_elementwise_fma(k, f32x2{b, b}, acc);
+  return;
+#elif defined(SFM_HARRIS_SCALAR_FMA)
+  acc.x = __builtin_fmaf(k.x, v[H], acc.x);
+  acc.y = __builtin_fmaf(k.y, v[H], acc.y);
   return;
 #endif
   if constexpr (H == 0)

@@ -3,8 +3,8 @@
 // kernel's waves share its CUs?
 //
 // Harris (the product kernel, compiled from sfmfromscratch_amd/csrc/harris.hip; built twice
-// by tools/Makefile: window fmas as inline-asm v_pk_fma_f32 and as the compiler's own packed
-// fmas, -DSFM_HARRIS_NATIVE_PK) runs on stream 1 over 32 synthetic 1080p planes, right after
+// by tools/Makefile: window fmas as inline-asm v_pk_fma_f32, as the compiler's own packed
+// fmas (-DSFM_HARRIS_NATIVE_PK) and as scalar v_fma_f32 (-DSFM_HARRIS_SCALAR_FMA)) runs on stream 1 over 32 synthetic 1080p planes, right after
 // a co-runner was launched on stream 2 with one 256-thread workgroup per CU (one wave per
 // SIMD, few VGPRs), so that every CU can hold one Harris workgroup beside it.  Each R map is
 // compared bit for bit with the R map of the same launch run alone.
@@ -98,8 +98,10 @@ int main(int argc, char** argv) {
   std::vector<std::string> kinds;
   for (int i = 3; i < argc; ++i) kinds.push_back(argv[i]);
   if (kinds.empty()) kinds = {"none", "mfma", "mfmal", "valu", "none"};
-#ifdef SFM_HARRIS_NATIVE_PK
+#if defined(SFM_HARRIS_NATIVE_PK)
   const char* variant = "native packed fma";
+#elif defined(SFM_HARRIS_SCALAR_FMA)
+  const char* variant = "scalar v_fma_f32 window sums";
 #else
   const char* variant = "inline-asm v_pk_fma_f32";
 #endif

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 counter passes on the headline bench: SQ issue/stall counters (tools/sq_summary.py)
+# Counter passes on the headline bench: SQ issue/stall counters (tools/sq_summary.py)
 # and HBM traffic (FETCH_SIZE, WRITE_SIZE in separate passes; tools/pmc_traffic.py).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
