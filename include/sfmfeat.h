@@ -241,6 +241,20 @@ int32_t sfm_match_pairs_prepped_dev(sfm_ctx* ctx, const float* desc, const int32
                                     float ratio, int32_t* matches, float* conf, int32_t* nmatch,
                                     void* stream);
 
+/* ---------------- batches in flight: the lane gate ----------------
+ * Replaces no reference interface: the reference runs one pair per host thread
+ * (Runner.py:183-191); this orders the device-resident batch path's lanes.  Contexts that
+ * share a gate (set with sfm_ctx_set_gate) serialise their extractions' Harris phases
+ * (pyramid, Harris and certified NMS of every level) in submission order: each batched
+ * extraction waits, on its stream, for the previous gated extraction's Harris phase, and
+ * its keypoint selection, descriptors (and the caller's matching) then overlap the next
+ * one's.  The gated contexts must be driven from one host thread; a gate must outlive the
+ * contexts that use it (or be unset with NULL first). */
+typedef struct sfm_gate sfm_gate;
+int32_t sfm_gate_create(int32_t device, sfm_gate** out);
+int32_t sfm_gate_destroy(sfm_gate* gate);
+int32_t sfm_ctx_set_gate(sfm_ctx* ctx, sfm_gate* gate);
+
 /* ---------------- stage profiling (bench.py's live roofline numbers) ----------------
  * When enabled, every stage's launches are bracketed by HIP events on the launch
  * stream; sfm_profile_read synchronises them and returns the accumulated device time

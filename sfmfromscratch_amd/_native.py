@@ -61,6 +61,9 @@ SIGNATURES = {
                                             ctypes.c_int32, _vp]),
     "sfm_match_pairs_prepped_dev": (ctypes.c_int32, [_vp, _vp, _vp, ctypes.c_int32, ctypes.c_int64, _vp,
                                                      ctypes.c_int32, ctypes.c_float, _vp, _vp, _vp, _vp]),
+    "sfm_gate_create": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(_vp)]),
+    "sfm_gate_destroy": (ctypes.c_int32, [_vp]),
+    "sfm_ctx_set_gate": (ctypes.c_int32, [_vp, _vp]),
     "sfm_profile_enable": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "sfm_profile_stages": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "sfm_profile_read": (ctypes.c_int32, [_vp, ctypes.POINTER(ctypes.c_double), _i64p, ctypes.c_int32]),
@@ -344,6 +347,32 @@ def debug_nms(R: np.ndarray, tnms, ksize: int = 3, tile: bool = False, device: i
     check(load_library().sfm_debug_nms(device, R.ctypes.data_as(_fp), B, H, W, ksize, t.ctypes.data,
                                        int(tile), keys.ctypes.data, cnt.ctypes.data_as(_i64p)))
     return [np.sort(keys[b * H * W: b * H * W + cnt[b]]) for b in range(B)]
+
+
+class Gate:
+    """sfm_gate: serialises the Harris phases of the contexts that share it (batches in
+    flight, pipeline.BatchPipeline)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = _vp()
+        if self.lib.sfm_gate_create(device, ctypes.byref(h)) != _abi.SFM_OK:
+            raise RuntimeError("sfm_gate_create failed: no usable MI355X (HIP) device")
+        self.handle = h
+
+    def attach(self, ctx: Context):
+        check(self.lib.sfm_ctx_set_gate(ctx.handle, self.handle), ctx.handle)
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            self.lib.sfm_gate_destroy(self.handle)
+            self.handle = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 _tls = threading.local()

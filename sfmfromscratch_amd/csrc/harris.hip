@@ -41,6 +41,13 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // acc = (k.x, k.y) * (v[H], v[H]) + acc : one v_pk_fma_f32 (two IEEE fmas, each bitwise
 // fmaf) with the product value broadcast to both halves by op_sel — no register shuffles.
+//
+// gfx950 hazard (tools/pk_mfma_hazard.hip, profiles/r04_pk_mfma_hazard.txt): a v_pk_fma_f32
+// whose LOW result reads src1's HIGH half (op_sel:[0,1,0]) returns wrong low results in lanes
+// 48-63 while an MFMA of another wave runs on the same SIMD.  The high-half broadcast is
+// therefore taken on src0 (op_sel:[1,0,0], product value first: a*b == b*a, so each half is
+// still bitwise fmaf(k, v, acc)); the low-half broadcast (op_sel_hi:[1,0,1]) is unaffected.
+// SFM_HARRIS_SRC1_HI (diagnostics builds only) restores the affected form.
 template <int H>
 __device__ __forceinline__ void pk_fma_bcast(f32x2& acc, f32x2 k, f32x2 v) {
 #if defined(SFM_HARRIS_NATIVE_PK)  // diagnostics builds only (tools/coresidency_repro.hip)
@@ -54,8 +61,13 @@ __device__ __forceinline__ void pk_fma_bcast(f32x2& acc, f32x2 k, f32x2 v) {
 #endif
   if constexpr (H == 0)
     asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "v"(k), "v"(v));
+#ifdef SFM_HARRIS_SRC1_HI
   else
     asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(k), "v"(v));
+#else
+  else
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(v), "v"(k));
+#endif
 }
 
 // One workgroup (2 per CU; see HarrisShape) walks 64 x 64 output tiles of one plane.

@@ -38,8 +38,19 @@ struct Level {
 
 }  // namespace
 
+// Lane gate (sfm_gate_*): the contexts of batches in flight share one; each extraction's
+// pyramid + Harris + certified-NMS phase starts after the previous gated extraction's phase
+// has finished, so those VALU-bound phases of two batches alternate instead of competing,
+// and each overlaps the other batch's keypoint selection, descriptors and matcher.
+struct sfm_gate {
+  int device = 0;
+  hipEvent_t ev = nullptr;  // end of the last gated Harris phase (timing disabled)
+  bool armed = false;       // ev has been recorded
+};
+
 struct sfm_ctx {
   int device = 0;
+  sfm_gate* gate = nullptr;
   sfm_params p;
   hipStream_t stream = nullptr;
   // extraction fork/join: keypoint selection + description of level l run on `aux` while
@@ -141,6 +152,13 @@ int ensure(sfm_ctx* c, DevBuf& b, size_t bytes) {
   b.bytes = 0;
   HIPCHK(c, hipMalloc(&b.p, bytes));
   b.bytes = bytes;
+  return SFM_OK;
+}
+
+// the stream of the host-pointer calls, created on first use
+int host_stream(sfm_ctx* c, hipStream_t* out) {
+  if (!c->stream) HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  *out = c->stream;
   return SFM_OK;
 }
 
@@ -250,6 +268,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   int rc = reserve_impl(c, B, H, W);
   if (rc) return rc;
   const int L = c->L;
+  if (c->gate && c->gate->armed) HIPCHK(c, hipStreamWaitEvent(st, c->gate->ev, 0));
   c->last_B = B;
   c->last_H = H;
   c->last_W = W;
@@ -401,6 +420,10 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
       }
     }
     l0 = l1;
+  }
+  if (c->gate) {  // this batch's Harris phase is done: the next gated extraction may start
+    HIPCHK(c, hipEventRecord(c->gate->ev, st));
+    c->gate->armed = true;
   }
   // the caller stream's levels: one selection launch for all of them (each level its own
   // scratch regions inside the stream's half), unless SFMFEAT_SELECT_MERGE=0
@@ -607,8 +630,10 @@ int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out) {
   int gs = p->gaussian_size;
   if (p->gauss_kernel_set) memcpy(c->gauss, p->gauss_kernel, sizeof(float) * gs * gs);
   else gaussian_taps(gs, p->sigma, c->gauss);
+  // the host-pointer calls' stream is created on first use (host_stream): a context that
+  // only serves the device-pointer batch path holds just its aux stream, so the HIP runtime's
+  // hardware queues (GPU_MAX_HW_QUEUES, 4 by default) go to streams that carry work
   bool ok = hipSetDevice(device) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess;
   for (hipEvent_t& e : c->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   if (!ok) {
@@ -752,7 +777,8 @@ int32_t sfm_ingest_rgb(sfm_ctx* c, const uint8_t* rgb, int32_t H, int32_t W, int
   int rc;
   if ((rc = ensure(c, c->i_rgb, (size_t)H * W * 3))) return rc;
   if ((rc = ensure(c, c->i_gray, (size_t)H2 * W2 * 4))) return rc;
-  hipStream_t st = c->stream;
+  hipStream_t st;
+  if ((rc = host_stream(c, &st))) return rc;
   HIPCHK(c, hipMemcpyAsync(c->i_rgb.p, rgb, (size_t)H * W * 3, hipMemcpyHostToDevice, st));
   if ((rc = ingest_impl(c, as<uint8_t>(c->i_rgb), 1, H, W, H2, W2, as<float>(c->i_gray), st))) return rc;
   HIPCHK(c, hipMemcpyAsync(gray, c->i_gray.p, (size_t)H2 * W2 * 4, hipMemcpyDeviceToHost, st));
@@ -887,7 +913,8 @@ int32_t sfm_ransac_find_inliers(sfm_ctx* c, const int64_t* p1, const int64_t* p2
   if ((rc = ensure(c, c->r_out, h.size() * 4))) return rc;
   if ((rc = ensure(c, c->r_on, 16))) return rc;
   if ((rc = ensure(c, c->r_oit, 16))) return rc;
-  hipStream_t st = c->stream;
+  hipStream_t st;
+  if ((rc = host_stream(c, &st))) return rc;
   const int32_t nn = (int32_t)n;
   HIPCHK(c, hipMemcpyAsync(c->r_pts.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, st));
   HIPCHK(c, hipMemcpyAsync(c->r_npts.p, &nn, 4, hipMemcpyHostToDevice, st));
@@ -925,7 +952,8 @@ int32_t sfm_extract(sfm_ctx* c, const float* img, int32_t H, int32_t W, int64_t 
   if ((rc = ensure(c, c->d_desc, (size_t)scap * 128 * 4))) return rc;
   if ((rc = ensure(c, c->d_count, 16))) return rc;
   if ((rc = ensure(c, c->d_conf, (size_t)scap * 4))) return rc;
-  hipStream_t st = c->stream;
+  hipStream_t st;
+  if ((rc = host_stream(c, &st))) return rc;
   HIPCHK(c, hipMemcpy2DAsync(c->d_img0.p, (size_t)W * 4, img, (size_t)row_stride * 4, (size_t)W * 4, H,
                              hipMemcpyHostToDevice, st));
   rc = extract_impl(c, as<float>(c->d_img0), 1, H, W, as<int32_t>(c->d_xy), as<float>(c->d_desc),
@@ -963,8 +991,9 @@ int32_t sfm_match(sfm_ctx* c, const float* d1, int64_t n1, const float* d2, int6
   HIPCHK(c, hipSetDevice(c->device));
   int64_t mcap = std::max(n1, n2);
   if (mcap > kMaxMatchRows) return set_err(c, SFM_EINVAL, "more than 16384 descriptors per side");
-  hipStream_t st = c->stream;
   int rc;
+  hipStream_t st;
+  if ((rc = host_stream(c, &st))) return rc;
   if ((rc = ensure(c, c->m_desc, (size_t)2 * mcap * 128 * 4))) return rc;
   if ((rc = ensure(c, c->m_count, 16))) return rc;
   if ((rc = ensure(c, c->m_pairs, 16))) return rc;
@@ -995,6 +1024,36 @@ int32_t sfm_match(sfm_ctx* c, const float* d1, int64_t n1, const float* d2, int6
     if (matches)
       for (int64_t i = 0; i < 2 * k; ++i) matches[i] = mm[i];
   }
+  return SFM_OK;
+}
+
+int32_t sfm_gate_create(int32_t device, sfm_gate** out) {
+  if (!out) return SFM_EINVAL;
+  *out = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return SFM_EDEVICE;
+  sfm_gate* g = new sfm_gate();
+  g->device = device;
+  if (hipEventCreateWithFlags(&g->ev, hipEventDisableTiming) != hipSuccess) {
+    delete g;
+    return SFM_EDEVICE;
+  }
+  *out = g;
+  return SFM_OK;
+}
+
+int32_t sfm_gate_destroy(sfm_gate* g) {
+  if (!g) return SFM_OK;
+  (void)hipSetDevice(g->device);
+  if (g->armed) (void)hipEventSynchronize(g->ev);
+  (void)hipEventDestroy(g->ev);
+  delete g;
+  return SFM_OK;
+}
+
+int32_t sfm_ctx_set_gate(sfm_ctx* c, sfm_gate* g) {
+  if (!c) return SFM_EINVAL;
+  if (g && g->device != c->device) return set_err(c, SFM_EINVAL, "gate and context on different devices");
+  c->gate = g;
   return SFM_OK;
 }
 

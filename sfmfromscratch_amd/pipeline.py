@@ -139,12 +139,21 @@ class BatchPipeline:
     every lane).
 
     `hook(slots, B)` runs on the lane's stream between extraction and matching (the halo
-    exchange of a sharded run, distributed.halo_exchange)."""
+    exchange of a sharded run, distributed.halo_exchange).
+
+    `gate` (default: SFMFEAT_LANE_GATE, off unless "1"): the lanes' contexts share one
+    sfm_gate, so batch i+1's pyramid / Harris / NMS phase starts when batch i's has ended and
+    overlaps batch i's selection, descriptors and matcher by construction, instead of by
+    whatever order the HIP runtime's shared hardware queues happen to give."""
 
     def __init__(self, extractor_params: dict | None, ratio_threshold: float, batch: int, H: int, W: int,
-                 pairs, inflight: int = 2, device: int = 0, extra_slots: int = 1):
+                 pairs, inflight: int = 2, device: int = 0, extra_slots: int = 1, gate: bool | None = None):
+        import os
+
         import torch
         self.torch = torch
+        if gate is None:
+            gate = os.environ.get("SFMFEAT_LANE_GATE", "0") == "1"
         self.B, self.H, self.W = batch, H, W
         self.inflight = max(1, int(inflight))
         self.pairs = pairs
@@ -166,6 +175,12 @@ class BatchPipeline:
                                "stream": torch.cuda.Stream(device=dev)})
         self.cap = self.lanes[0]["ex"].cap
         self.n = 0
+        self.gate = None
+        if gate and self.inflight > 1:
+            from ._native import Gate
+            self.gate = Gate(device)
+            for ln in self.lanes:
+                self.gate.attach(ln["ex"].ctx)
 
     @property
     def contexts(self):

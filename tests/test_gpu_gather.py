@@ -187,10 +187,11 @@ def test_chunked_job_1080p_concurrent_matching_equals_clean_extraction():
         assert not bad, f"{len(bad)} gathered slots differ from a clean extraction: {bad[:10]}"
 
 
-def test_pipeline_1080p_lanes_equal_clean_extraction():
+@pytest.mark.parametrize("gate", [False, True])
+def test_pipeline_1080p_lanes_equal_clean_extraction(gate):
     """The headline pipeline (two 32 x 1080p batches in flight, each lane's matcher overlapping
-    the other lane's extraction): every lane's slots after every batch equal a clean
-    single-frame extraction."""
+    the other lane's extraction; with and without the lane gate): every lane's slots after
+    every batch equal a clean single-frame extraction."""
     torch = pytest.importorskip("torch")
     from sfmfromscratch_amd import distributed as D
     from sfmfromscratch_amd.pipeline import BatchPipeline, consecutive_pairs
@@ -199,7 +200,7 @@ def test_pipeline_1080p_lanes_equal_clean_extraction():
     ref = _clean_checksums(torch, u8)
     frames = torch.from_numpy(synth.u8_to_gray(u8.cpu().numpy())).cuda()
     pairs = torch.from_numpy(consecutive_pairs(B)).cuda()
-    pipe = BatchPipeline(P_1080, RATIO, B, 1080, 1920, pairs, inflight=2, extra_slots=1)
+    pipe = BatchPipeline(P_1080, RATIO, B, 1080, 1920, pairs, inflight=2, extra_slots=1, gate=gate)
     cks = []
     for _ in range(6):
         ln = pipe.submit(frames)

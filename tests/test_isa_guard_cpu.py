@@ -1,0 +1,65 @@
+"""CPU: the built libsfmfeat.so contains no instruction form known to return wrong results
+on gfx950 while an MFMA of another wave runs on the same SIMD.
+
+tools/pk_mfma_hazard.hip measured it (profiles/r04_pk_mfma_hazard.txt, DESIGN.md §7
+*Co-residency*): `v_pk_fma_f32` whose low result reads src1's high half (op_sel bit 1 set)
+returns wrong low results in lanes 48-63 beside a registers-only MFMA co-runner; the other
+packed-FP32 forms measured clean.  The product runs Harris (packed fmas) and the matcher
+(MFMA) of two batches at once, so a compiler or source change that brings the form back must
+fail here, on the CPU, before any GPU run.
+
+The device code objects are read from the library's .hip_fatbin section (one offload bundle
+per translation unit) with the ROCm LLVM tools; the test skips when they are missing."""
+from __future__ import annotations
+
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "sfmfromscratch_amd", "lib", "libsfmfeat.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+# (instruction, op_sel pattern) pairs measured to misbehave beside MFMA
+FORBIDDEN = [("v_pk_fma_f32", re.compile(r"op_sel:\[[01],1,[01]\]"))]
+
+
+def _device_asm(tmp_path) -> str:
+    objcopy = shutil.which("objcopy")
+    bundler, objdump = os.path.join(LLVM, "clang-offload-bundler"), os.path.join(LLVM, "llvm-objdump")
+    if not (os.path.exists(LIB) and objcopy and os.path.exists(bundler) and os.path.exists(objdump)):
+        pytest.skip("library or ROCm LLVM tools not available")
+    fb = tmp_path / "fatbin.bin"
+    subprocess.run([objcopy, "-O", "binary", "--only-section=.hip_fatbin", LIB, str(fb)], check=True)
+    data = fb.read_bytes()
+    starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
+    assert starts, "no offload bundle in .hip_fatbin"
+    out = []
+    for n, i in enumerate(starts):
+        j = starts[n + 1] if n + 1 < len(starts) else len(data)
+        b, e = tmp_path / f"b{n}.bin", tmp_path / f"b{n}.elf"
+        b.write_bytes(data[i:j])
+        subprocess.run([bundler, "--unbundle", "--type=o", f"--input={b}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={e}"], check=True)
+        out.append(subprocess.run([objdump, "-d", "--mcpu=gfx950", str(e)], check=True,
+                                  capture_output=True, text=True).stdout)
+    return "\n".join(out)
+
+
+def test_no_packed_fma_with_src1_high_half_select(tmp_path):
+    asm = _device_asm(tmp_path)
+    assert "v_pk_fma_f32" in asm and "v_mfma" in asm  # the scan sees both kernels' code
+    bad, kernel = [], None
+    for line in asm.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.*)>:", line)
+        if m:
+            kernel = m.group(1)
+            continue
+        for op, pat in FORBIDDEN:
+            if op in line and pat.search(line):
+                bad.append(f"{kernel}: {line.split('//')[0].strip()}")
+    assert not bad, f"{len(bad)} hazardous instructions, e.g. {bad[:3]}"

@@ -3,7 +3,7 @@
 # twice, interleaved); prints img/s, ms/step and the per-stage ms of every run.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   i=0
   for e in "$@"; do
     i=$((i+1))

@@ -102,8 +102,10 @@ int main(int argc, char** argv) {
   const char* variant = "native packed fma";
 #elif defined(SFM_HARRIS_SCALAR_FMA)
   const char* variant = "scalar v_fma_f32 window sums";
+#elif defined(SFM_HARRIS_SRC1_HI)
+  const char* variant = "inline-asm v_pk_fma_f32, high-half broadcast on src1 (op_sel:[0,1,0], round 3)";
 #else
-  const char* variant = "inline-asm v_pk_fma_f32";
+  const char* variant = "inline-asm v_pk_fma_f32, high-half broadcast on src0 (op_sel:[1,0,0])";
 #endif
   const int64_t n = (int64_t)B * H * W;
   float *d_img, *d_ref, *d_R, *d_g, *d_sink;

@@ -14,6 +14,13 @@
 //     3 v_pk_mul_f32
 //     4 v_pk_add_f32
 //     5 v_fma_f32 pairs (scalar control)
+//     6 v_pk_fma_f32 op_sel:[1,0,0] op_sel_hi:[1,1,1] (src0's high half broadcast)
+//     7 v_pk_fma_f32 op_sel:[0,1,0] op_sel_hi:[1,0,1] (src1's halves swapped)
+//     8 v_pk_mul_f32 op_sel:[0,1] op_sel_hi:[1,1] (src1's high half broadcast)
+//     9 v_pk_add_f32 op_sel:[0,1] op_sel_hi:[1,1] (src1's high half broadcast)
+//    10 v_pk_mul_f32 op_sel_hi:[1,0] (src1's low half broadcast)
+//    11 v_pk_fma_f32 op_sel:[0,0,1] op_sel_hi:[1,1,1] (src2's high half broadcast)
+//    12 v_pk_mov_b32 op_sel:[1,0] (src0's high half into the low result), then v_pk_add_f32
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -41,6 +48,23 @@ __device__ __forceinline__ void step(f32x2& a, f32x2 k, f32x2 v) {
   if constexpr (OP == 2) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(a) : "v"(k), "v"(v));
   if constexpr (OP == 3) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(a) : "v"(k));
   if constexpr (OP == 4) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(a) : "v"(v));
+  if constexpr (OP == 6)
+    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(a) : "v"(v), "v"(k));
+  if constexpr (OP == 7)
+    asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,0,1]" : "+v"(a) : "v"(k), "v"(v));
+  if constexpr (OP == 8) asm volatile("v_pk_mul_f32 %0, %0, %1 op_sel:[0,1] op_sel_hi:[1,1]" : "+v"(a) : "v"(k));
+  if constexpr (OP == 9) asm volatile("v_pk_add_f32 %0, %0, %1 op_sel:[0,1] op_sel_hi:[1,1]" : "+v"(a) : "v"(v));
+  if constexpr (OP == 10) asm volatile("v_pk_mul_f32 %0, %0, %1 op_sel_hi:[1,0]" : "+v"(a) : "v"(k));
+  if constexpr (OP == 11) {
+    f32x2 t = a;
+    asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,1,1]" : "=v"(a) : "v"(k), "v"(v), "v"(t));
+    a.x = a.x * 0.5f;  // keep the chain bounded
+  }
+  if constexpr (OP == 12) {
+    f32x2 t;
+    asm volatile("v_pk_mov_b32 %0, %1, %1 op_sel:[1,0]" : "=v"(t) : "v"(a));
+    asm volatile("v_pk_add_f32 %0, %1, %2" : "=v"(a) : "v"(t), "v"(v));
+  }
   if constexpr (OP == 5) {
     asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a.x) : "v"(k.x), "v"(v.x));
     asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a.y) : "v"(k.y), "v"(v.y));
@@ -53,8 +77,9 @@ __global__ void __launch_bounds__(256) k_ops(int iters, float* out) {
   f32x2 acc[8];
   for (int i = 0; i < 8; ++i) acc[i] = f32x2{1e-3f * (t % 977) + i, 2e-3f * (t % 613) - i};
   // products stay near 1 (mul), sums grow slowly (add: +1e-7 per step), fmas converge
-  const f32x2 k = OP == 3 ? f32x2{0.9999999f, 1.0000001f} : f32x2{0.5f, 0.25f};
-  const f32x2 v = OP == 4 ? f32x2{1e-7f, -1e-7f} : f32x2{0.75f, 1.5f};
+  const bool mul = OP == 3 || OP == 8 || OP == 10, add = OP == 4 || OP == 9 || OP == 12;
+  const f32x2 k = mul ? f32x2{0.9999999f, 1.0000001f} : f32x2{0.5f, 0.25f};
+  const f32x2 v = add ? f32x2{1e-7f, -1e-7f} : f32x2{0.75f, 1.5f};
   for (int it = 0; it < iters; ++it)
 #pragma unroll
     for (int i = 0; i < 8; ++i) step<OP>(acc[i], k, v);
@@ -96,14 +121,22 @@ int main(int argc, char** argv) {
   hipStream_t s1, s2;
   CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
-  const char* names[6] = {"v_pk_fma_f32 op_sel_hi:[1,0,1]", "v_pk_fma_f32 op_sel:[0,1,0]", "v_pk_fma_f32",
-                          "v_pk_mul_f32", "v_pk_add_f32", "v_fma_f32 (scalar)"};
-  void (*launch[6])(int, int, float*, hipStream_t) = {launch_ops<0>, launch_ops<1>, launch_ops<2>,
-                                                      launch_ops<3>, launch_ops<4>, launch_ops<5>};
+  constexpr int NOPS = 13;
+  const char* names[NOPS] = {"v_pk_fma_f32 op_sel_hi:[1,0,1]", "v_pk_fma_f32 op_sel:[0,1,0]", "v_pk_fma_f32",
+                             "v_pk_mul_f32", "v_pk_add_f32", "v_fma_f32 (scalar)",
+                             "v_pk_fma_f32 op_sel:[1,0,0]", "v_pk_fma_f32 op_sel:[0,1,0] hi:[1,0,1]",
+                             "v_pk_mul_f32 op_sel:[0,1]", "v_pk_add_f32 op_sel:[0,1]",
+                             "v_pk_mul_f32 op_sel_hi:[1,0]", "v_pk_fma_f32 op_sel:[0,0,1]",
+                             "v_pk_mov_b32 op_sel:[1,0] + v_pk_add_f32"};
+  void (*launch[NOPS])(int, int, float*, hipStream_t) = {
+      launch_ops<0>, launch_ops<1>, launch_ops<2>, launch_ops<3>, launch_ops<4>, launch_ops<5>,
+      launch_ops<6>, launch_ops<7>, launch_ops<8>, launch_ops<9>, launch_ops<10>, launch_ops<11>,
+      launch_ops<12>};
   std::vector<float> ref(n), got(n);
   printf("pk_mfma_hazard: %d ops workgroups x 256 threads x %d iterations x 8 chains; co-runner %d x 256 "
          "threads, %d MFMAs each\n", nwg, iters, ncu, co_iters);
-  for (int op = 0; op < 6; ++op) {
+  const int op0 = argc > 3 ? atoi(argv[3]) : 0;
+  for (int op = op0; op < NOPS; ++op) {
     launch[op](nwg, iters, d_ref, s1);
     CK(hipStreamSynchronize(s1));
     CK(hipMemcpy(ref.data(), d_ref, n * 4, hipMemcpyDeviceToHost));
@@ -123,7 +156,7 @@ int main(int argc, char** argv) {
             ++half_bad[i % 2];
           }
         }
-        printf("  %-32s %s rep %d: %lld of %zu results differ (.x %lld, .y %lld)", names[op],
+        printf("  %-40s %s rep %d: %lld of %zu results differ (.x %lld, .y %lld)", names[op],
                co ? "beside MFMA" : "alone      ", rep, bad, n, half_bad[0], half_bad[1]);
         if (bad) {
           printf("; lanes:");
