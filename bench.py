@@ -683,14 +683,21 @@ def run_gather(args, torch, dist, dev, rank, world):
         t_compute = timed(job, frames, max(2, min(args.steps, 10)), exchange=False)
         sent = S * job.slot_bytes
         if not job.halo:
+            # bytes of the last (timed-shape) run: count-compacted rows, against full slots
+            recv, recv_full = job.gathered_bytes()
             t_alone = job.gather_alone()
-            gathered = n_global * job.slot_bytes
-            recv = (world - 1) * sent
+            gathered = recv * world // (world - 1)
+            sent = recv // (world - 1)
             bound = recv / ((world - 1) * XGMI_LINK_GBS * 1e9)
-            comm = {"kind": ("one grouped all_gather_into_tensor (desc|xy|count) per chunk" if job.coalesce
-                             else "all_gather_into_tensor x3 fields per chunk") + f" ({dist.get_backend()})",
-                    "chunks": C, "bytes_sent_per_rank": sent, "bytes_gathered_per_rank": gathered,
-                    "bytes_received_per_rank": recv, "ms_alone": round(t_alone * 1e3, 3),
+            kind = ("count-compacted: counts, then each chunk's first M rows (M = its largest count), "
+                    if job.compact else "full-capacity slots, ")
+            kind += ("grouped all_gather_into_tensor per chunk" if job.coalesce else "one all_gather_into_tensor "
+                     "per field per chunk") + f" ({dist.get_backend()})"
+            comm = {"kind": kind, "chunks": C, "bytes_sent_per_rank": sent, "bytes_gathered_per_rank": gathered,
+                    "bytes_received_per_rank": recv, "bytes_received_full_slots": recv_full,
+                    "padding_bytes_saved_per_rank": recv_full - recv,
+                    "rows_per_chunk_mean": round(float(np.mean(job.gathered_rows)), 1) if job.gathered_rows else None,
+                    "ms_alone": round(t_alone * 1e3, 3),
                     "algbw_GBps": round(gathered / t_alone / 1e9, 1),
                     "xgmi_bound_ms": round(bound * 1e3, 3), "xgmi_bound_frac": round(bound / t_alone, 3),
                     "xgmi_bound_note": f"received bytes over (N-1) xGMI links at {XGMI_LINK_GBS:.0f} GB/s each "

@@ -242,21 +242,80 @@ def allgather_chunk(dist, table, plan: GatherPlan, c: int, src, async_op: bool =
     return works
 
 
+class CompactStage:
+    """Staging buffers of the count-compacted chunk gather (allgather_chunk_compact): the
+    packed send rows and the gathered [world * chunk, M, ...] rows before they are unpacked
+    into the table."""
+
+    def __init__(self, torch, world: int, chunk: int, cap: int, device):
+        self.send_desc = torch.empty((chunk * cap * 128,), dtype=torch.float32, device=device)
+        self.send_xy = torch.empty((chunk * cap * 2,), dtype=torch.int32, device=device)
+        self.recv_desc = torch.empty((world * chunk * cap * 128,), dtype=torch.float32, device=device)
+        self.recv_xy = torch.empty((world * chunk * cap * 2,), dtype=torch.int32, device=device)
+
+
+def allgather_chunk_counts(dist, table, plan: GatherPlan, c: int, src, async_op: bool = False, group=None):
+    """Phase 1 of the count-compacted gather: chunk c's keypoint counts (4 B per frame) into
+    the table's count field."""
+    bc, base = plan.chunk_size(c), plan.chunk_base(c)
+    w = dist.all_gather_into_tensor(table.count[base:base + plan.world * bc], src.count[:bc], group=group,
+                                    async_op=async_op)
+    return [w] if async_op else []
+
+
+def allgather_chunk_rows(dist, table, plan: GatherPlan, c: int, src, stage: CompactStage, M: int,
+                         group=None, coalesce: bool = False):
+    """Phase 2: the first M rows (M = the chunk's largest count over every rank, read on the
+    host after phase 1) of every slot's desc and xy — the rows a count-aware reader (the
+    matcher's prep, the checksums) ever reads — packed per rank, gathered and unpacked into
+    the table's [slot, :M] rows, on the caller's current stream.  Returns the work handles
+    of the collectives (async) and the bytes each rank received."""
+    bc, base = plan.chunk_size(c), plan.chunk_base(c)
+    n = plan.world * bc
+    if M <= 0:
+        return [], 0
+    sd = stage.send_desc[:bc * M * 128].view(bc, M, 128)
+    sx = stage.send_xy[:bc * M * 2].view(bc, M, 2)
+    sd.copy_(src.desc[:bc, :M])
+    sx.copy_(src.xy[:bc, :M])
+    rd = stage.recv_desc[:n * M * 128]
+    rx = stage.recv_xy[:n * M * 2]
+    if coalesce:
+        with dist._coalescing_manager(group, async_ops=True) as cm:
+            dist.all_gather_into_tensor(rd, sd.view(-1), group=group)
+            dist.all_gather_into_tensor(rx, sx.view(-1), group=group)
+        works = [cm]
+    else:
+        works = [dist.all_gather_into_tensor(rd, sd.view(-1), group=group, async_op=True),
+                 dist.all_gather_into_tensor(rx, sx.view(-1), group=group, async_op=True)]
+    for w in works:  # the unpack waits for the gather on the current stream (RCCL: no host wait)
+        w.wait()
+    table.desc[base:base + n, :M].copy_(rd.view(n, M, 128))
+    table.xy[base:base + n, :M].copy_(rx.view(n, M, 2))
+    return works, (plan.world - 1) * bc * M * (128 * 4 + 2 * 4)
+
+
 def slot_checksums(torch, slots, idx=None):
     """[n, 3] int64 per-slot checksums (desc bits, xy, count; each a position-weighted sum,
     so a moved or permuted slot changes it) of slots `idx` (default: all) — exact integer
-    arithmetic on the device, used to verify the exchange bit for bit."""
+    arithmetic on the device, used to verify the exchange bit for bit.  Only rows below the
+    slot's count enter (the rows any reader of the table uses; the count-compacted gather
+    moves no others)."""
     if idx is None:
         idx = torch.arange(slots.count.shape[0], device=slots.count.device)
     out = []
+    cap = slots.desc.shape[1]
     for a in range(0, idx.shape[0], 64):  # bounded int64 temporaries
         i = idx[a:a + 64]
         n = i.shape[0]
-        db = slots.desc[i].reshape(n, -1).view(torch.int32).to(torch.int64)
+        cnt = slots.count[i].to(torch.int64)
+        live = (torch.arange(cap, device=cnt.device)[None, :] < cnt[:, None]).to(torch.int64)  # rows < count
+        db = slots.desc[i].view(torch.int32).to(torch.int64) * live[:, :, None]
+        db = db.reshape(n, -1)
         w = torch.arange(1, db.shape[1] + 1, device=db.device, dtype=torch.int64)
-        xb = slots.xy[i].reshape(n, -1).to(torch.int64)
+        xb = (slots.xy[i].to(torch.int64) * live[:, :, None]).reshape(n, -1)
         wx = torch.arange(1, xb.shape[1] + 1, device=xb.device, dtype=torch.int64)
-        out.append(torch.stack([(db * w).sum(1), (xb * wx).sum(1), slots.count[i].to(torch.int64)], dim=1))
+        out.append(torch.stack([(db * w).sum(1), (xb * wx).sum(1), cnt], dim=1))
     if not out:
         return torch.zeros((0, 3), dtype=torch.int64, device=slots.count.device)
     return torch.cat(out)
@@ -285,7 +344,7 @@ class ChunkedGatherJob:
 
     def __init__(self, extractor_params: dict | None, ratio: float, plan: GatherPlan, rank: int, H: int, W: int,
                  dist=None, inflight: int = 2, exchange: str = "allgather", device: int = 0, group=None,
-                 coalesce: bool | None = None, keep_all_results: bool = False):
+                 coalesce: bool | None = None, keep_all_results: bool = False, compact: bool | None = None):
         import torch
         from .pipeline import BatchExtractor, BatchMatcher, SlotTable
         self.torch, self.plan, self.rank, self.dist, self.group = torch, plan, rank, dist, group
@@ -329,6 +388,13 @@ class ChunkedGatherJob:
                 self.rank_pairs_n = len(rp)
         for ln in self.lanes:
             ln["slots"] = SlotTable(torch, Bx, cap, dev) if world > 1 and not self.halo else None
+        # count-compacted gather (default on for the multi-rank all-gather; SFM_GATHER_COMPACT=0
+        # gathers full-capacity slots): counts first, then only each chunk's first M rows
+        if compact is None:
+            compact = os.environ.get("SFM_GATHER_COMPACT", "1") != "0"
+        self.compact = bool(compact) and world > 1 and not self.halo
+        self.stage = CompactStage(torch, world, Bx, cap, dev) if self.compact else None
+        self.gathered_rows = []  # per chunk of the last run: M (compact) or cap
         self.CH = 4096  # 'all': pairs per matcher launch
         self.keep_all_results = bool(keep_all_results)
         if self.sched is not None:
@@ -363,7 +429,12 @@ class ChunkedGatherJob:
         """Enqueue one job over this rank's frames [S, H, W] (u8 or f32, device-resident).
         exchange=False skips the collectives (timing of the compute alone: the matcher then
         reads whatever the table holds).  record_sent keeps per-frame checksums of the slots
-        this rank sends (`verify_exchange`)."""
+        this rank sends (`verify_exchange`).
+
+        With the count-compacted gather, chunk c's counts are gathered right after its
+        extraction; its rows are gathered once the host has read the chunk's largest count,
+        which happens after chunk c+1's extraction was enqueued (one host wait per chunk,
+        with the next chunk already queued on the GPU)."""
         torch, plan, dist = self.torch, self.plan, self.dist
         world, rank, Bx, C = plan.world, self.rank, plan.chunk, plan.C
         assert frames.shape[0] == plan.S and frames.is_cuda and frames.is_contiguous()
@@ -374,6 +445,53 @@ class ChunkedGatherJob:
             ln["stream"].wait_stream(cur)
             ln["pending"] = None
         self.mstream.wait_stream(cur)
+        if exchange:  # rows gathered per chunk by this run (gathered_bytes)
+            self.gathered_rows = []
+        compact = self.compact and exchange
+        waiting = []  # compact: chunks whose counts are in flight, (c, lane, count works)
+
+        def match_chunk(c, works, ln, ready=None):
+            """Prep chunk c's slots and match its ready pairs on the matcher stream, after the
+            chunk's collectives (`works`), its unpack (`ready` event) or its lane."""
+            if self.sched is None:
+                return
+            bc, l0 = plan.chunk_size(c), c * Bx
+            with torch.cuda.stream(self.mstream):
+                if ready is not None:
+                    self.mstream.wait_event(ready)
+                elif works:
+                    for w in works:
+                        w.wait()
+                elif self.halo and c == C - 1:  # the halo slot arrived on chunk 0's lane
+                    for other in self.lanes:
+                        self.mstream.wait_stream(other["stream"])
+                else:
+                    self.mstream.wait_stream(ln["stream"])
+                # this chunk's slots get their matcher operands once; pairs of earlier
+                # chunks' slots reuse theirs
+                if self.halo:
+                    self.matcher.prep(self.table, l0, bc + (1 if c == C - 1 and world > 1 else 0))
+                else:
+                    self.matcher.prep(self.table, plan.chunk_base(c), world * bc)
+                if len(self.sched[c]):
+                    self.matcher.match(self.table, self.sched_dev[c], out=self.outs[c], prepped=True)
+
+        def finish_compact(c, ln, cworks):
+            # the chunk's largest count over every rank (host wait on its count gather), then
+            # its first M rows: gathered and unpacked on the lane's stream
+            bc, base = plan.chunk_size(c), plan.chunk_base(c)
+            with torch.cuda.stream(ln["stream"]):
+                for w in cworks:
+                    w.wait()
+                M = int(self.table.count[base:base + world * bc].max().item()) if bc else 0
+                works, _ = allgather_chunk_rows(dist, self.table, plan, c, ln["slots"], self.stage, M,
+                                                group=self.group, coalesce=self.coalesce)
+                ln["pending"] = works
+                done = torch.cuda.Event()
+                done.record(ln["stream"])  # the unpacked rows are in the table
+            self.gathered_rows.append(M)
+            match_chunk(c, None, ln, ready=done)
+
         for c in range(C):
             ln = self.lanes[c % len(self.lanes)]
             bc = plan.chunk_size(c)
@@ -395,28 +513,22 @@ class ChunkedGatherJob:
                     if record_sent:
                         g0 = plan.local_frames(rank, c)[0]
                         self.sent_ck[g0:g0 + bc] = slot_checksums(torch, self._view(ln["slots"], 0, bc))
-                    if exchange:
+                    if compact:
+                        cworks = allgather_chunk_counts(dist, self.table, plan, c, ln["slots"], async_op=True,
+                                                        group=self.group)
+                    elif exchange:
                         works = self.gather_chunk(c, ln["slots"])
                         ln["pending"] = works
-            if self.sched is None:
+                        self.gathered_rows.append(self.cap)
+            if compact:
+                # chunk c - 1's counts: read after chunk c was enqueued
+                while waiting:
+                    finish_compact(*waiting.pop(0))
+                waiting.append((c, ln, cworks))
                 continue
-            with torch.cuda.stream(self.mstream):
-                if works:
-                    for w in works:
-                        w.wait()
-                elif self.halo and c == C - 1:  # the halo slot arrived on chunk 0's lane
-                    for other in self.lanes:
-                        self.mstream.wait_stream(other["stream"])
-                else:
-                    self.mstream.wait_stream(ln["stream"])
-                # this chunk's slots get their matcher operands once; pairs of earlier
-                # chunks' slots reuse theirs
-                if self.halo:
-                    self.matcher.prep(self.table, l0, bc + (1 if c == C - 1 and world > 1 else 0))
-                else:
-                    self.matcher.prep(self.table, plan.chunk_base(c), world * bc)
-                if len(self.sched[c]):
-                    self.matcher.match(self.table, self.sched_dev[c], out=self.outs[c], prepped=True)
+            match_chunk(c, works, ln)
+        while waiting:
+            finish_compact(*waiting.pop(0))
         for ln in self.lanes:
             cur.wait_stream(ln["stream"])
             if ln["pending"]:
@@ -440,19 +552,40 @@ class ChunkedGatherJob:
             self.pairs_matched = len(mine)
             self.last_all_pairs = sp
 
+    def gathered_bytes(self) -> tuple[int, int]:
+        """(bytes each rank received in the last run's row gathers, the same at full slot
+        capacity): the padding the count-compacted gather saved is their difference."""
+        plan = self.plan
+        per_row = 128 * 4 + 2 * 4
+        got = full = 0
+        for c, M in enumerate(self.gathered_rows):
+            bc = plan.chunk_size(c)
+            got += (plan.world - 1) * bc * (M * per_row + 4)
+            full += (plan.world - 1) * bc * (self.cap * per_row + 4)
+        return got, full
+
     def gather_alone(self, reps: int = 3) -> float:
-        """Seconds per job of the chunked all-gather with nothing else on the GPU (host-timed
-        between barriers)."""
+        """Seconds per job of the chunked exchange with nothing else on the GPU (host-timed
+        between barriers), in the form the job runs (count-compacted: counts, the host read of
+        each chunk's M, rows, unpack; else full-capacity slots), on lane 0's last slots."""
         import time
-        torch, dist = self.torch, self.dist
+        torch, dist, plan = self.torch, self.dist, self.plan
         src = self.lanes[0]["slots"]
         dist.barrier(group=self.group)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
-            for c in range(self.plan.C):
-                for w in self.gather_chunk(c, src):
-                    w.wait()
+            for c in range(plan.C):
+                if self.compact:
+                    for w in allgather_chunk_counts(dist, self.table, plan, c, src, async_op=True, group=self.group):
+                        w.wait()
+                    bc, base = plan.chunk_size(c), plan.chunk_base(c)
+                    M = int(self.table.count[base:base + plan.world * bc].max().item())
+                    allgather_chunk_rows(dist, self.table, plan, c, src, self.stage, M, group=self.group,
+                                         coalesce=self.coalesce)
+                else:
+                    for w in self.gather_chunk(c, src):
+                        w.wait()
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / reps
 

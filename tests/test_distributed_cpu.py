@@ -55,6 +55,41 @@ def _worker(rank, world, port, n_global, mode, errq):
             else:
                 assert int(slots.count[n_local]) == 0  # untouched
             glob = [(lo + int(i), lo + int(j)) for i, j in pairs]
+        elif mode.startswith("compact"):  # the count-compacted chunk gather (counts, then M rows)
+            plan = D.GatherPlan(n_global, world, 3, "consecutive")
+            table = SlotTable(torch, n_global, CAP, "cpu")
+            src = SlotTable(torch, plan.chunk, CAP, "cpu")
+            stage = D.CompactStage(torch, world, plan.chunk, CAP, "cpu")
+            moved = 0
+            for c in range(plan.C):
+                lo, hi = plan.local_frames(rank, c)
+                for b, g in enumerate(range(lo, hi)):
+                    _fill_slot(src, b, g)
+                    src.desc[b, int(src.count[b]):] = -7.0 - rank  # rows past the count: not live
+                    src.xy[b, int(src.count[b]):] = -7 - rank
+                for w in D.allgather_chunk_counts(dist, table, plan, c, src, async_op=True):
+                    w.wait()
+                bc, base = plan.chunk_size(c), plan.chunk_base(c)
+                M = int(table.count[base:base + world * bc].max())
+                assert M == max(3 + g % 7 for r in range(world) for g in range(*plan.local_frames(r, c)))
+                _, nb = D.allgather_chunk_rows(dist, table, plan, c, src, stage, M)
+                moved += nb
+            for g in range(n_global):  # every frame's live rows at slot_of(g), bit-equal
+                ref = SlotTable(torch, 1, CAP, "cpu")
+                _fill_slot(ref, 0, g)
+                s, n = int(plan.slot_of(g)), int(ref.count[0])
+                assert int(table.count[s]) == n
+                assert torch.equal(table.desc[s, :n], ref.desc[0, :n]) and torch.equal(table.xy[s, :n], ref.xy[0, :n])
+                Mg = max(3 + h % 7 for h in range(n_global) if plan.chunk_of(h) == plan.chunk_of(g))
+                assert not table.desc[s, Mg:].any()  # rows past the chunk's M are never sent
+            ck = D.slot_checksums(torch, table, torch.from_numpy(plan.slot_of(np.arange(n_global)).astype(np.int64)))
+            for g in range(n_global):  # checksums see only the live rows
+                ref = SlotTable(torch, 1, CAP, "cpu")
+                _fill_slot(ref, 0, g)
+                ref.desc[0, int(ref.count[0]):] = 123.0
+                assert torch.equal(ck[g], D.slot_checksums(torch, ref)[0])
+            assert 0 < moved < (world - 1) * plan.S * CAP * (128 * 4 + 8)
+            glob = []  # no pairs in this mode
         elif mode.startswith("plan"):  # configs[3]: chunked all-gather (distributed.GatherPlan)
             sched_name = mode.split("/", 1)[1]
             plan = D.GatherPlan(n_global, world, 3, sched_name)
@@ -102,7 +137,7 @@ def _worker(rank, world, port, n_global, mode, errq):
             glob = [tuple(map(int, p)) for p in D.all_pairs_for_rank(n_global, rank, world)]
         gathered = [None] * world
         dist.all_gather_object(gathered, glob)
-        if rank == 0:
+        if rank == 0 and not mode.startswith("compact"):
             allp = sorted(p for g in gathered for p in g)
             if mode in ("halo", "plan/consecutive"):
                 expect = [(i, i + 1) for i in range(n_global - 1)]
@@ -155,6 +190,15 @@ def test_chunked_allgather_plan(world, n_global, sched):
     slot on every rank; the ranks' pairs cover the global schedule exactly once, each in a
     chunk at which both of its frames are gathered."""
     _run(world, n_global, "plan/" + sched)
+
+
+@pytest.mark.parametrize("world,n_global", [(2, 16), (3, 21)])
+def test_count_compacted_chunk_gather(world, n_global):
+    """The count-compacted gather (counts first, then each chunk's first M rows, M = its
+    largest count over the ranks): every frame's live rows land bit-equal at its slot, rows
+    past a count are never sent, checksums cover the live rows only, and fewer bytes move
+    than with full-capacity slots."""
+    _run(world, n_global, "compact")
 
 
 def test_gather_plan_layout_and_weighted_deal():
