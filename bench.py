@@ -369,8 +369,10 @@ def main():
         timing event per step on its lane's stream right after its match (the step's end)."""
         pipe.start()
         for _ in range(nsteps):
+            h0 = time.perf_counter()
             step()
             if step_events is not None:
+                host_ms.append((time.perf_counter() - h0) * 1e3)
                 e = torch.cuda.Event(enable_timing=True)
                 e.record(pipe.lanes[(pipe.n - 1) % pipe.inflight]["stream"])
                 step_events.append(e)
@@ -384,7 +386,7 @@ def main():
     torch.cuda.synchronize()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    step_ev = []
+    step_ev, host_ms = [], []
     if dom and args.events_in_timed:  # A/B: the per-launch events inside the timed region
         for c in ctxs:
             c.profile_stages([dom])
@@ -410,7 +412,9 @@ def main():
                    "steady_ms_per_step": (round((step_end[-1] - step_end[len(step_end) // 2]) /
                                                 max(1, len(step_end) - 1 - len(step_end) // 2), 4)
                                           if len(step_end) > 2 else None),
-                   "host_submit_ms": round(t_sub * 1e3, 3)}
+                   "host_submit_ms": round(t_sub * 1e3, 3),
+                   "host_step_submit_ms_max": round(max(host_ms), 3) if host_ms else None,
+                   "host_step_submit_ms_median": round(float(np.median(host_ms)), 3) if host_ms else None}
 
     # the roofline: the same two-lane pipeline again, K steps, with HIP events around each
     # launch of the dominant stage (kept out of the timed region above)

@@ -244,12 +244,12 @@ int32_t sfm_match_pairs_prepped_dev(sfm_ctx* ctx, const float* desc, const int32
 /* ---------------- batches in flight: the lane gate ----------------
  * Replaces no reference interface: the reference runs one pair per host thread
  * (Runner.py:183-191); this orders the device-resident batch path's lanes.  Contexts that
- * share a gate (set with sfm_ctx_set_gate) serialise their extractions' Harris phases
- * (pyramid, Harris and certified NMS of every level) in submission order: each batched
- * extraction waits, on its stream, for the previous gated extraction's Harris phase, and
- * its keypoint selection, descriptors (and the caller's matching) then overlap the next
- * one's.  The gated contexts must be driven from one host thread; a gate must outlive the
- * contexts that use it (or be unset with NULL first). */
+ * share a gate (set with sfm_ctx_set_gate) order their extractions in submission order:
+ * each batched extraction's pyramid waits, on its stream, until the previous gated
+ * extraction's level-0 Harris launch has finished, so the two batches' largest VALU
+ * launches never compete, and one batch's level-0 Harris overlaps the other's level-0 NMS,
+ * selection and descriptors.  The gated contexts must be driven from one host thread; a
+ * gate must outlive the contexts that use it (or be unset with NULL first). */
 typedef struct sfm_gate sfm_gate;
 int32_t sfm_gate_create(int32_t device, sfm_gate** out);
 int32_t sfm_gate_destroy(sfm_gate* gate);

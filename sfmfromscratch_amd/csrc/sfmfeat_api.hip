@@ -39,12 +39,12 @@ struct Level {
 }  // namespace
 
 // Lane gate (sfm_gate_*): the contexts of batches in flight share one; each extraction's
-// pyramid + Harris + certified-NMS phase starts after the previous gated extraction's phase
-// has finished, so those VALU-bound phases of two batches alternate instead of competing,
-// and each overlaps the other batch's keypoint selection, descriptors and matcher.
+// pyramid starts after the previous gated extraction's level-0 Harris launch has finished
+// (SFMFEAT_GATE_LEVEL moves the release point), so the two batches' largest VALU launches
+// alternate instead of competing for the CUs.
 struct sfm_gate {
   int device = 0;
-  hipEvent_t ev = nullptr;  // end of the last gated Harris phase (timing disabled)
+  hipEvent_t ev = nullptr;  // release point of the last gated extraction (timing disabled)
   bool armed = false;       // ev has been recorded
 };
 
@@ -379,6 +379,22 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     const char* e = getenv("SFMFEAT_HARRIS_GROUP");
     return e ? atoi(e) : 0;
   }();
+  // the lane gate's release point: after the Harris launch of level gate_level (default 0:
+  // the next gated extraction's pyramid and level-0 Harris follow this one's level-0 Harris;
+  // SFMFEAT_GATE_LEVEL=-1: after every level's Harris and NMS)
+  static const int gate_level = [] {
+    const char* e = getenv("SFMFEAT_GATE_LEVEL");
+    return e ? atoi(e) : 0;
+  }();
+  bool gate_released = false;
+  auto release_gate = [&]() -> int {
+    if (c->gate && !gate_released) {
+      HIPCHK(c, hipEventRecord(c->gate->ev, st));
+      c->gate->armed = true;
+      gate_released = true;
+    }
+    return SFM_OK;
+  };
   for (int l0 = 0; l0 < L;) {
     int l1 = l0 + 1;
     if (group_from > 0 && l0 >= group_from) l1 = std::min(L, l0 + kHarrisMaxLevels);
@@ -398,6 +414,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
       }
       launch_harris_levels(g, B, as<float>(c->d_gauss), c->p.gaussian_size, alpha, st);
     }
+    if (gate_level >= l0 && gate_level < l1 && (rc = release_gate())) return rc;
     for (int l = l0; l < l1; ++l) {
       const LevelBufs& e = lb[l];
       if (!e.exact) {
@@ -421,10 +438,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     }
     l0 = l1;
   }
-  if (c->gate) {  // this batch's Harris phase is done: the next gated extraction may start
-    HIPCHK(c, hipEventRecord(c->gate->ev, st));
-    c->gate->armed = true;
-  }
+  if ((rc = release_gate())) return rc;  // (SFMFEAT_GATE_LEVEL=-1, or fewer levels)
   // the caller stream's levels: one selection launch for all of them (each level its own
   // scratch regions inside the stream's half), unless SFMFEAT_SELECT_MERGE=0
   static const bool merge_select = [] {

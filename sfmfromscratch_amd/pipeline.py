@@ -142,9 +142,9 @@ class BatchPipeline:
     exchange of a sharded run, distributed.halo_exchange).
 
     `gate` (default: SFMFEAT_LANE_GATE, off unless "1"): the lanes' contexts share one
-    sfm_gate, so batch i+1's pyramid / Harris / NMS phase starts when batch i's has ended and
-    overlaps batch i's selection, descriptors and matcher by construction, instead of by
-    whatever order the HIP runtime's shared hardware queues happen to give."""
+    sfm_gate, so batch i+1's pyramid and level-0 Harris start when batch i's level-0 Harris
+    has ended and overlap batch i's level-0 NMS, selection and descriptors by construction,
+    instead of by whatever order the HIP runtime's shared hardware queues happen to give."""
 
     def __init__(self, extractor_params: dict | None, ratio_threshold: float, batch: int, H: int, W: int,
                  pairs, inflight: int = 2, device: int = 0, extra_slots: int = 1, gate: bool | None = None):
