@@ -301,7 +301,129 @@ __global__ void __launch_bounds__(NT) k_nms_stream(const float* __restrict__ R,
   }
 }
 
+// k_nms_band (the default certified 3x3 form since round 4): as k_nms_stream, but each
+// thread walks NB strips of 8 rows down its column group, carrying the last two rows' values
+// and horizontal maxima from one strip to the next in registers, so every row of R is read
+// once per band instead of 10 / 8 times (the strips' halo rows: PMC traffic 1.36x the
+// algorithmic bytes).  Candidates of the whole band are appended with one
+// atomic per workgroup (flag words: 32 bits per strip).
+template <int NB, int NT>
+__global__ void __launch_bounds__(NT) k_nms_band(const float* __restrict__ R, const MedianState* __restrict__ st,
+                                                  uint64_t* __restrict__ cand,
+                                                  unsigned long long* __restrict__ cand_count, int H, int W,
+                                                  int nbands) {
+  constexpr int SH = 8;
+  static_assert(NB >= 1 && NB <= 4, "two 64-bit flag words");
+  const int b = blockIdx.y;
+  if (st[b].fallback != 0) return;  // whole workgroup: fallback planes take the exact path
+  const uint32_t tnms = st[b].tnms;
+  const int64_t n = (int64_t)H * W;
+  const float* Rp = R + (int64_t)b * n;
+  const int C4 = W >> 2;
+  const int lane = threadIdx.x & 63;
+  __shared__ uint32_t s_wsum[NT / 64];
+  __shared__ unsigned long long s_base;
+  const int64_t groups = (int64_t)C4 * nbands;
+  const int64_t nvb = (groups + NT - 1) / NT;
+  for (int64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+    const int64_t gid = vb * NT + threadIdx.x;
+    const bool active = gid < groups;
+    const int g = active ? (int)gid : (int)(groups - 1);  // inactive lanes mirror the last group
+    const int band = g / C4, c4 = g - band * C4;
+    const int ytop = band * NB * SH;  // first output row of the band
+    const float* colp = Rp + 4 * c4;
+    const bool need_l = lane == 0 && c4 > 0, need_r = lane == 63 && c4 < C4 - 1;
+    const int eoff = need_l ? -1 : 4;
+    // one image row of this column group: its 4 values (-inf outside the image) and the
+    // horizontal max3 of each column (outer neighbours from the adjacent lanes / the edge load)
+    auto hrow = [&](const float4& v0, float e, bool rowok, float4& v, float (&h)[4]) {
+      v = rowok ? v0 : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      const float up = __shfl_up(v.w, 1), dn = __shfl_down(v.x, 1);
+      float l = c4 == 0 ? -INFINITY : (lane == 0 ? e : up);
+      float r = c4 == C4 - 1 ? -INFINITY : (lane == 63 ? e : dn);
+      if (!rowok) l = r = -INFINITY;
+      h[0] = fmaxf(fmaxf(l, v.x), v.y);
+      h[1] = fmaxf(fmaxf(v.x, v.y), v.z);
+      h[2] = fmaxf(fmaxf(v.y, v.z), v.w);
+      h[3] = fmaxf(fmaxf(v.z, v.w), r);
+    };
+    auto load = [&](int y, float4& v, float& e) {
+      const int gy = min(max(y, 0), H - 1);
+      v = *reinterpret_cast<const float4*>(colp + (int64_t)gy * W);
+      e = (need_l || need_r) ? colp[(int64_t)gy * W + eoff] : -INFINITY;
+    };
+    // carried rows: a = row y - 1, c = row y (values and horizontal maxima)
+    float4 va, vc;
+    float ha[4], hc[4];
+    {
+      float4 r0, r1;
+      float e0, e1;
+      load(ytop - 1, r0, e0);
+      load(ytop, r1, e1);
+      hrow(r0, e0, ytop - 1 >= 0 && ytop - 1 < H, va, ha);
+      hrow(r1, e1, ytop < H, vc, hc);
+    }
+    uint64_t flags0 = 0ull, flags1 = 0ull;
+#pragma unroll 1
+    for (int sb = 0; sb < NB; ++sb) {  // not unrolled: one strip's registers at a time
+      const int y0 = ytop + sb * SH;  // output rows y0 .. y0 + 7 need image rows up to y0 + 8
+      float4 raw[SH];
+      float er[SH];
+      uint32_t strip = 0;  // 4 bits per output row of this strip
+#pragma unroll
+      for (int j = 0; j < SH; ++j) load(y0 + 1 + j, raw[j], er[j]);  // every load in flight
+#pragma unroll
+      for (int j = 0; j < SH; ++j) {
+        float4 vn;
+        float hn[4];
+        const int yn = y0 + 1 + j;
+        hrow(raw[j], er[j], yn < H, vn, hn);
+        // output row y = yn - 1: centre vc, window rows a (y - 1), c (y), n (y + 1)
+        const int y = yn - 1;
+        const bool inside = active && y < H;
+        const float cv[4] = {vc.x, vc.y, vc.z, vc.w};
+        uint32_t fr = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float m = fmaxf(fmaxf(ha[e], hc[e]), hn[e]);
+          const bool pred = inside && fkey(cv[e]) >= tnms && cv[e] == m;
+          fr |= pred ? (1u << (4 * j + e)) : 0u;
+        }
+        strip |= fr;
+        va = vc;
+        vc = vn;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ha[e] = hc[e];
+          hc[e] = hn[e];
+        }
+      }
+      const uint64_t sw = (uint64_t)strip << (32 * (sb & 1));
+      if (sb < 2) flags0 |= sw;
+      else flags1 |= sw;
+    }
+    const uint64_t flags[2] = {flags0, flags1};
+    const uint32_t nf = (uint32_t)(__popcll(flags[0]) + __popcll(flags[1]));
+    if (!__syncthreads_or(nf != 0)) continue;
+    const int64_t slot = block_append(&cand_count[(int64_t)b * kCounterStride], nf, s_wsum, &s_base);
+    if (nf == 0) continue;
+    uint64_t* out = cand + (int64_t)b * n + slot;
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      uint64_t f = flags[w];
+      while (f) {  // the few candidates re-read their value (an L2 hit)
+        const int bit = __builtin_ctzll(f);
+        f &= f - 1;
+        const int sb = 2 * w + (bit >> 5), j = (bit & 31) >> 2;
+        const uint32_t idx = (uint32_t)((ytop + sb * SH + j) * W + 4 * c4 + (bit & 3));
+        *out++ = ((uint64_t)(~fkey(Rp[idx])) << 32) | idx;
+      }
+    }
+  }
+}
+
 constexpr int kStreamSH = 8;
+constexpr int kBandStrips = 4;  // strips of 8 rows per k_nms_band thread (SFMFEAT_NMS_BAND=0: k_nms_stream)
 
 static bool nms_tile_forced() {  // SFMFEAT_NMS_TILE=1: the tiled kernel for mode 0 too (A/B)
   static const bool f = [] {
@@ -390,6 +512,20 @@ static void launch_tile(const float* R, const MedianState* state, uint64_t* cand
     // of R ahead of the real one (timing only: how fast R reads once Harris's writes drained)
     static const int sh = [] { const char* e = getenv("SFMFEAT_NMS_SH"); return e ? atoi(e) : kStreamSH; }();
     static const bool dry = [] { const char* e = getenv("SFMFEAT_NMS_DRY"); return e && atoi(e) != 0; }();
+    static const int band = [] { const char* e = getenv("SFMFEAT_NMS_BAND"); return e ? atoi(e) : kBandStrips; }();
+    if (band >= 1 && band <= 4 && !dry) {
+      const int rows = 8 * band;
+      const int nbands = (H + rows - 1) / rows;
+      const int64_t nvb = ((int64_t)(W >> 2) * nbands + 255) / 256;
+      dim3 grid((unsigned)nvb, B);
+      switch (band) {
+        case 1: hipLaunchKernelGGL((k_nms_band<1, 256>), grid, dim3(256), 0, st, R, state, cand, cnt, H, W, nbands); break;
+        case 2: hipLaunchKernelGGL((k_nms_band<2, 256>), grid, dim3(256), 0, st, R, state, cand, cnt, H, W, nbands); break;
+        case 3: hipLaunchKernelGGL((k_nms_band<3, 256>), grid, dim3(256), 0, st, R, state, cand, cnt, H, W, nbands); break;
+        default: hipLaunchKernelGGL((k_nms_band<4, 256>), grid, dim3(256), 0, st, R, state, cand, cnt, H, W, nbands); break;
+      }
+      return;
+    }
     const int SHr = (sh == 4 || sh == 16) ? sh : kStreamSH;
     const int NTr = 256;
     const int nstrips = (H + SHr - 1) / SHr;
