@@ -181,7 +181,7 @@ def main():
     ap.add_argument("--rgb-ingest", action="store_true",
                     help="c2: frames resident as decoded 2x-size RGB (3840x2160x3 u8); each step first runs "
                          "FeatureRunner's ingest on the device (PIL BICUBIC x0.5 + _rgb2gray, Runner.py:33-46)")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=int(os.environ.get("BENCH_INFLIGHT", "2")),
                     help="batches in flight (double-buffered contexts / slot tables, pipeline.BatchPipeline)")
     ap.add_argument("--verify", action="store_true",
                     help="c4: after the timed run, re-extract a sample of frames and re-match a sample of this "

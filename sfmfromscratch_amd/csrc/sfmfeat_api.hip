@@ -649,6 +649,10 @@ int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out) {
   // hardware queues (GPU_MAX_HW_QUEUES, 4 by default) go to streams that carry work
   bool ok = hipSetDevice(device) == hipSuccess &&
             hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess;
+  {  // SFMFEAT_EAGER_HOST_STREAM=1 (A/B): the round-3 stream layout (host stream made here)
+    const char* e = getenv("SFMFEAT_EAGER_HOST_STREAM");
+    if (ok && e && atoi(e) == 1) ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+  }
   for (hipEvent_t& e : c->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   if (!ok) {
     if (c->stream) (void)hipStreamDestroy(c->stream);

@@ -2,9 +2,10 @@
 on gfx950 while an MFMA of another wave runs on the same SIMD.
 
 tools/pk_mfma_hazard.hip measured it (profiles/r04_pk_mfma_hazard.txt, DESIGN.md §7
-*Co-residency*): `v_pk_fma_f32` whose low result reads src1's high half (op_sel bit 1 set)
-returns wrong low results in lanes 48-63 beside a registers-only MFMA co-runner; the other
-packed-FP32 forms measured clean.  The product runs Harris (packed fmas) and the matcher
+*Co-residency*): a packed-FP32 instruction (`v_pk_fma_f32`, `v_pk_mul_f32`, `v_pk_add_f32`)
+whose low result reads src1's high half (op_sel bit 1 set) returns wrong low results in lanes
+48-63 beside a registers-only MFMA co-runner; the forms without it (no op_sel, src0's or
+src2's high half, src1's low half broadcast by op_sel_hi) measured clean.  The product runs Harris (packed fmas) and the matcher
 (MFMA) of two batches at once, so a compiler or source change that brings the form back must
 fail here, on the CPU, before any GPU run.
 
@@ -24,8 +25,11 @@ LIB = os.path.join(ROOT, "sfmfromscratch_amd", "lib", "libsfmfeat.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
-# (instruction, op_sel pattern) pairs measured to misbehave beside MFMA
-FORBIDDEN = [("v_pk_fma_f32", re.compile(r"op_sel:\[[01],1,[01]\]"))]
+# (instruction, op_sel pattern) pairs measured to misbehave beside MFMA: every packed-FP32
+# form whose low result takes src1's high half (profiles/r04_pk_mfma_hazard.txt)
+FORBIDDEN = [("v_pk_fma_f32", re.compile(r"op_sel:\[[01],1,[01]\]")),
+             ("v_pk_mul_f32", re.compile(r"op_sel:\[[01],1\]")),
+             ("v_pk_add_f32", re.compile(r"op_sel:\[[01],1\]"))]
 
 
 def _device_asm(tmp_path) -> str:
