@@ -351,15 +351,6 @@ def main():
                 ach = amount / (ms / 1e3)
                 st.update({"bound": bound, "achieved": round(ach, 3), "unit": unit, "frac": round(ach / peak, 4)})
             stages[k] = st
-        lvl_kp = level_keypoints()
-        if lvl_kp is not None and "describe" in stages:
-            fl_ms, ops = describe_floor(lvl_kp, nprof)
-            d = stages["describe"]
-            d.update({"bound": "valu", "achieved": round(ops / (prof_all["describe"][0] / 1e3) / 1e12, 3),
-                      "unit": "T lane-op/s", "floor_ms_per_step": round(fl_ms / nprof, 4),
-                      "frac": round(fl_ms / prof_all["describe"][0], 4),
-                      "keypoints_per_level": [int(v) for v in lvl_kp],
-                      "note": "modelled lane-ops per keypoint (bench.describe_ops) / 39.3 T lane-op/s"})
         dom = max((k for k in prof_all if k in work and prof_all[k][1]), key=lambda k: prof_all[k][0])
         prof_enable(False)
         prof_read()
@@ -415,6 +406,20 @@ def main():
                    "host_submit_ms": round(t_sub * 1e3, 3),
                    "host_step_submit_ms_max": round(max(host_ms), 3) if host_ms else None,
                    "host_step_submit_ms_median": round(float(np.median(host_ms)), 3) if host_ms else None}
+
+    # the describe floor's keypoint counts: a host-path extraction (PCIe copies, the GPU
+    # mostly idle), so after the timed region rather than between the profile pass and the
+    # warm-up, where it would let the GPU's clocks drop right before timing
+    if stages and "describe" in stages:
+        lvl_kp = level_keypoints()
+        if lvl_kp is not None:
+            fl_ms, ops = describe_floor(lvl_kp, nprof)
+            d = stages["describe"]
+            d.update({"bound": "valu", "achieved": round(ops / (prof_all["describe"][0] / 1e3) / 1e12, 3),
+                      "unit": "T lane-op/s", "floor_ms_per_step": round(fl_ms / nprof, 4),
+                      "frac": round(fl_ms / prof_all["describe"][0], 4),
+                      "keypoints_per_level": [int(v) for v in lvl_kp],
+                      "note": "modelled lane-ops per keypoint (bench.describe_ops) / 39.3 T lane-op/s"})
 
     # the roofline: the same two-lane pipeline again, K steps, with HIP events around each
     # launch of the dominant stage (kept out of the timed region above)
