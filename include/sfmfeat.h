@@ -241,6 +241,18 @@ int32_t sfm_match_pairs_prepped_dev(sfm_ctx* ctx, const float* desc, const int32
                                     float ratio, int32_t* matches, float* conf, int32_t* nmatch,
                                     void* stream);
 
+/* ---------------- stream layout of a context ----------------
+ * Replaces no reference interface (the reference has no device streams).
+ * sfm_ctx_stream: the context's own HIP stream (created on first use; the host-pointer calls
+ * run on it) for callers that enqueue the batch calls on it instead of a stream of their own.
+ * sfm_ctx_set_serial: 1 = extractions run every stage on the caller's stream (no internal
+ * aux stream, no fork/join); 0 = the two largest levels' selection and descriptors overlap
+ * the later levels' Harris on the context's aux stream (default; SFMFEAT_SERIAL=1 flips the
+ * default).  Each stream maps onto one of the HIP runtime's hardware queues, and streams
+ * beyond GPU_MAX_HW_QUEUES share one, so a batch pipeline chooses how many it uses. */
+int32_t sfm_ctx_stream(sfm_ctx* ctx, void** stream);
+int32_t sfm_ctx_set_serial(sfm_ctx* ctx, int32_t serial);
+
 /* ---------------- batches in flight: the lane gate ----------------
  * Replaces no reference interface: the reference runs one pair per host thread
  * (Runner.py:183-191); this orders the device-resident batch path's lanes.  Contexts that

@@ -61,6 +61,8 @@ SIGNATURES = {
                                             ctypes.c_int32, _vp]),
     "sfm_match_pairs_prepped_dev": (ctypes.c_int32, [_vp, _vp, _vp, ctypes.c_int32, ctypes.c_int64, _vp,
                                                      ctypes.c_int32, ctypes.c_float, _vp, _vp, _vp, _vp]),
+    "sfm_ctx_stream": (ctypes.c_int32, [_vp, ctypes.POINTER(_vp)]),
+    "sfm_ctx_set_serial": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "sfm_gate_create": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(_vp)]),
     "sfm_gate_destroy": (ctypes.c_int32, [_vp]),
     "sfm_ctx_set_gate": (ctypes.c_int32, [_vp, _vp]),
@@ -187,6 +189,16 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    def stream(self) -> int:
+        """The context's own HIP stream (hipStream_t as an int), created on first use."""
+        h = _vp()
+        check(self.lib.sfm_ctx_stream(self.handle, ctypes.byref(h)), self.handle)
+        return int(h.value or 0)
+
+    def set_serial(self, serial: bool):
+        """Every extraction stage on the caller's stream (no aux-stream overlap)."""
+        check(self.lib.sfm_ctx_set_serial(self.handle, 1 if serial else 0), self.handle)
 
     def select_stats(self):
         """(planes that took the exact-median path, planes) of the last extraction."""

@@ -323,10 +323,15 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   // `aux`, overlapping the later levels' Harris; the small levels' selection and
   // descriptors run on the caller's stream once its Harris work is done.  Descriptors of
   // level l need the keypoint counts of levels < l (slot offsets): ev[L + 2 + l].
-  hipStream_t ax = c->aux;
-  const int L_aux = c->serial ? 0 : std::min(L, 2);  // SFMFEAT_SERIAL=1: one stream (isolated timings)
-  HIPCHK(c, hipEventRecord(c->ev[L], st));
-  HIPCHK(c, hipStreamWaitEvent(ax, c->ev[L], 0));
+  // serial (SFMFEAT_SERIAL=1 or sfm_ctx_set_serial): one stream, no fork/join at all
+  const int L_aux = c->serial ? 0 : std::min(L, 2);
+  hipStream_t ax = nullptr;
+  if (L_aux > 0) {
+    if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));  // on first use
+    ax = c->aux;
+    HIPCHK(c, hipEventRecord(c->ev[L], st));
+    HIPCHK(c, hipStreamWaitEvent(ax, c->ev[L], 0));
+  }
   const int rotate = c->p.mode == SFM_MODE_NAIVE ? 0 : 1;
   struct LevelBufs {
     float* R;
@@ -463,9 +468,10 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   }
   if (L_aux > 0 && L > L_aux) HIPCHK(c, hipStreamWaitEvent(st, c->ev[L + 2], 0));
   for (int l = L_aux; l < L; ++l) describe_level(l, st);
-  // join: the caller's stream waits for the aux work
-  HIPCHK(c, hipEventRecord(c->ev[L + 1], ax));
-  HIPCHK(c, hipStreamWaitEvent(st, c->ev[L + 1], 0));
+  if (L_aux > 0) {  // join: the caller's stream waits for the aux work
+    HIPCHK(c, hipEventRecord(c->ev[L + 1], ax));
+    HIPCHK(c, hipStreamWaitEvent(st, c->ev[L + 1], 0));
+  }
   if (!counted) launch_finalize_counts(as<int32_t>(c->d_lc), B, L, count, st);
   HIPCHK(c, hipGetLastError());
   return SFM_OK;
@@ -644,14 +650,17 @@ int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out) {
   int gs = p->gaussian_size;
   if (p->gauss_kernel_set) memcpy(c->gauss, p->gauss_kernel, sizeof(float) * gs * gs);
   else gaussian_taps(gs, p->sigma, c->gauss);
-  // the host-pointer calls' stream is created on first use (host_stream): a context that
-  // only serves the device-pointer batch path holds just its aux stream, so the HIP runtime's
-  // hardware queues (GPU_MAX_HW_QUEUES, 4 by default) go to streams that carry work
-  bool ok = hipSetDevice(device) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess;
-  {  // SFMFEAT_EAGER_HOST_STREAM=1 (A/B): the round-3 stream layout (host stream made here)
+  // Both streams are created on first use: the context's own stream (host-pointer calls,
+  // sfm_ctx_stream) and the aux stream (non-serial extractions).  The HIP runtime maps streams
+  // onto GPU_MAX_HW_QUEUES hardware queues (4 by default) and streams beyond that share one,
+  // which serialises them; a context that only carries work on the streams it needs keeps
+  // the caller's stream layout under the caller's control (pipeline.BatchPipeline).
+  bool ok = hipSetDevice(device) == hipSuccess;
+  {  // SFMFEAT_EAGER_HOST_STREAM=1 (A/B): the round-3 stream layout (both made here)
     const char* e = getenv("SFMFEAT_EAGER_HOST_STREAM");
-    if (ok && e && atoi(e) == 1) ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
+    if (ok && e && atoi(e) == 1)
+      ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+           hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess;
   }
   for (hipEvent_t& e : c->ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   if (!ok) {
@@ -664,8 +673,8 @@ int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out) {
   }
   if (ensure(c, c->d_gauss, sizeof(float) * gs * gs) ||
       hipMemcpy(c->d_gauss.p, c->gauss, sizeof(float) * gs * gs, hipMemcpyHostToDevice) != hipSuccess) {
-    (void)hipStreamDestroy(c->stream);
-    (void)hipStreamDestroy(c->aux);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
     delete c;
     return SFM_EDEVICE;
@@ -1042,6 +1051,22 @@ int32_t sfm_match(sfm_ctx* c, const float* d1, int64_t n1, const float* d2, int6
     if (matches)
       for (int64_t i = 0; i < 2 * k; ++i) matches[i] = mm[i];
   }
+  return SFM_OK;
+}
+
+int32_t sfm_ctx_set_serial(sfm_ctx* c, int32_t serial) {
+  if (!c) return SFM_EINVAL;
+  c->serial = serial != 0;
+  return SFM_OK;
+}
+
+int32_t sfm_ctx_stream(sfm_ctx* c, void** stream) {
+  if (!c || !stream) return SFM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipStream_t st;
+  int rc;
+  if ((rc = host_stream(c, &st))) return rc;
+  *stream = (void*)st;
   return SFM_OK;
 }
 

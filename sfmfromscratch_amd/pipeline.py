@@ -147,22 +147,41 @@ class BatchPipeline:
     instead of by whatever order the HIP runtime's shared hardware queues happen to give."""
 
     def __init__(self, extractor_params: dict | None, ratio_threshold: float, batch: int, H: int, W: int,
-                 pairs, inflight: int = 2, device: int = 0, extra_slots: int = 1, gate: bool | None = None):
+                 pairs, inflight: int = 2, device: int = 0, extra_slots: int = 1, gate: bool | None = None,
+                 lane_streams: str | None = None, serial_lanes=None):
         import os
 
         import torch
         self.torch = torch
         if gate is None:
             gate = os.environ.get("SFMFEAT_LANE_GATE", "0") == "1"
+        # lane_streams: "torch" (a stream from torch's pool per lane) or "context" (the lane
+        # context's own stream, wrapped as a torch ExternalStream: no torch stream pool, so
+        # the process's streams are exactly the lanes' and the HIP runtime's hardware-queue
+        # mapping of them follows their creation order).  serial_lanes: lane indices whose
+        # extraction runs on one stream (sfm_ctx_set_serial), e.g. "0" in SFMFEAT_SERIAL_LANES
+        if lane_streams is None:
+            lane_streams = os.environ.get("SFMFEAT_LANE_STREAMS", "torch")
+        if serial_lanes is None:
+            env = os.environ.get("SFMFEAT_SERIAL_LANES", "")
+            serial_lanes = [int(v) for v in env.replace("+", ",").split(",") if v.strip()]
+        self.lane_streams = lane_streams
+        self.serial_lanes = sorted(set(int(v) for v in serial_lanes))
         self.B, self.H, self.W = batch, H, W
         self.inflight = max(1, int(inflight))
         self.pairs = pairs
         dev = torch.device("cuda", device)
         P = int(pairs.shape[0])
         self.lanes = []
-        for _ in range(self.inflight):
+        for li in range(self.inflight):
             ex = BatchExtractor(extractor_params, device=device)
             ex.reserve(batch, H, W)
+            if li in self.serial_lanes:
+                ex.ctx.set_serial(True)
+            if lane_streams == "context":
+                stream = torch.cuda.ExternalStream(ex.ctx.stream(), device=dev)
+            else:
+                stream = torch.cuda.Stream(device=dev)
             m = BatchMatcher(ratio_threshold, device=device, ctx=ex.ctx)
             slots = SlotTable(torch, batch + extra_slots, ex.cap, dev)
             view = SlotTable.__new__(SlotTable)
@@ -171,8 +190,7 @@ class BatchPipeline:
             mout = (torch.zeros((max(P, 1), max(ex.cap, 1), 2), dtype=torch.int32, device=dev),
                     torch.zeros((max(P, 1), max(ex.cap, 1)), dtype=torch.float32, device=dev),
                     torch.zeros((max(P, 1),), dtype=torch.int32, device=dev))
-            self.lanes.append({"ex": ex, "m": m, "slots": slots, "view": view, "mout": mout,
-                               "stream": torch.cuda.Stream(device=dev)})
+            self.lanes.append({"ex": ex, "m": m, "slots": slots, "view": view, "mout": mout, "stream": stream})
         self.cap = self.lanes[0]["ex"].cap
         self.n = 0
         self.gate = None

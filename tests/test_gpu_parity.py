@@ -269,18 +269,21 @@ def test_1080p_batch_consistency_and_golden():
         assert np.array_equal(bits(desc[b, :n]), bits(desc[f, :n]))
 
 
-@pytest.mark.parametrize("gate", [False, True])
-def test_pipeline_batches_in_flight_match_serial(gate):
-    """pipeline.BatchPipeline (2 batches in flight on separate contexts/streams, with and
-    without the lane gate that serialises their Harris phases) gives the same slots and
-    matches as one BatchExtractor/BatchMatcher run per batch."""
+@pytest.mark.parametrize("gate,lane_streams,serial_lanes", [(False, "torch", []), (True, "torch", []),
+                                                            (False, "context", [0]), (True, "context", [0, 1])])
+def test_pipeline_batches_in_flight_match_serial(gate, lane_streams, serial_lanes):
+    """pipeline.BatchPipeline (2 batches in flight on separate contexts/streams; with and
+    without the lane gate, on torch pool streams or the contexts' own streams, lanes with
+    and without the aux-stream overlap) gives the same slots and matches as one
+    BatchExtractor/BatchMatcher run per batch."""
     torch = pytest.importorskip("torch")
     from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, BatchPipeline, consecutive_pairs
     B, H, W = 4, 270, 480
     pp = dict(P_OCT, num_interest_points=600)
     batches = [torch.from_numpy(synth.make_batch_u8(B, H, W, seed=300 + i)).cuda() for i in range(3)]
     pairs = torch.from_numpy(consecutive_pairs(B)).cuda()
-    pipe = BatchPipeline(pp, 0.85, B, H, W, pairs, inflight=2, extra_slots=0, gate=gate)
+    pipe = BatchPipeline(pp, 0.85, B, H, W, pairs, inflight=2, extra_slots=0, gate=gate, lane_streams=lane_streams,
+                         serial_lanes=serial_lanes)
     assert (pipe.gate is not None) == gate
     lanes = [pipe.submit(f) for f in batches]
     pipe.join()
