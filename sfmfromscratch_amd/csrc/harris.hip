@@ -36,6 +36,9 @@ constexpr int kHT = 64;   // output tile columns (rows: HarrisShape::TH, 64 or 3
 constexpr int kHarrisSmallTiles = 4;
 // 1: the 7 x 7 window's default form keeps product planes in LDS (form 3; SFMFEAT_HARRIS_PP)
 constexpr int kHarrisProductPlanes = 0;
+// 1: the 7 x 7 window's large levels sum their windows on MFMA (form 4; SFMFEAT_HARRIS_MF,
+// 2 = every level)
+constexpr int kHarrisMfma = 0;
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -106,10 +109,14 @@ __device__ int64_t g_harris_stamps_cap;  // u64 slots behind g_harris_stamps (wo
 //      product planes Ix^2, Iy^2, IxIy (the image tile aliased into them) instead of the two
 //      gradient planes, so the window phase reads products instead of re-forming them for
 //      every row it feeds (each gradient row's products were formed by 2.5 threads).
+//   4: the window sums on the matrix pipe (v_mfma_f32_4x4x1_16b_f32, see "MFMA window"
+//      below): 256 threads, 64 x 64 tiles, 2 workgroups per CU; wave w owns tile columns
+//      16w .. 16w+15 and lane l tile row l.
 template <int F>
 struct HarrisShape {
   static constexpr bool PP = F == 3;                     // product planes in LDS
-  static constexpr int NPAIR = (F == 0 || F == 3) ? 2 : 1;  // output row pairs per thread
+  static constexpr bool MF = F == 4;                     // window sums on MFMA
+  static constexpr int NPAIR = (F == 0 || F == 3 || F == 4) ? 2 : 1;  // output row pairs per thread
   static constexpr int NT = F == 1 ? 512 : 256;          // threads per workgroup
   static constexpr int RPT = 2 * NPAIR;                  // output rows per thread
   static constexpr int TH = RPT * 4 * (NT / 64);         // tile rows (tile columns: kHT)
@@ -117,11 +124,39 @@ struct HarrisShape {
   static constexpr int WPE = WPC * NT / 256;             // waves per SIMD
 };
 
+// MFMA window (form 4).  v_mfma_f32_4x4x1_16b_f32 is 16 independent 4 x 4 outer products
+// per instruction, D[lane 4b+j][reg i] += A[lane 4b+i] * B[lane 4b+j], and its result is
+// bitwise a k-ordered fmaf chain (tools/mfma_f32_probe.hip, profiles/r04_mfma_f32_probe.txt:
+// 0 of 256 results differ over chains of 1 .. 4096 steps).  A horizontal window row is a
+// banded (Toeplitz) product: for a 4-column strip at tile columns x .. x+3, step s = 0 ..
+// KS+2 takes gradient column x + s (B: the product at that column in the lane's row) and the
+// tap g[dy][s - i] for output column x + i (A: 0 outside the band).  Each output pixel then
+// sees its taps in row-major order with zero taps in between, and fmaf(0, p, acc) == acc
+// for finite p and acc != -0 (acc starts at +0 and a sum of finite values never rounds to
+// -0), so the chain is the reference's.  7 of every 10 MACs are taps at KS = 7.
+template <int KS>
+struct MfWin {
+  static constexpr int NS = KS + 3;              // steps per tap row (4 columns + KS - 1)
+  static constexpr int NC = 12 + NS;             // gradient columns a wave reads per row (4 strips)
+  static constexpr int NB4 = (NC + 3) / 4;       // b128 LDS reads per row per plane
+  // row stride: >= the tile's gradient columns and the last wave's reads, stride/4 odd
+  // (ds_read_b128 lane groups of 16 rows then hit 16 distinct 16-B slots)
+  static constexpr int stride() {
+    int s = kHT + KS - 1;
+    if (s < 48 + 4 * NB4) s = 48 + 4 * NB4;
+    s = (s + 3) / 4 * 4;
+    if (((s / 4) & 1) == 0) s += 4;
+    return s;
+  }
+};
+
 template <int KS, bool VEC, int ABL = 0, int F = 0>
 __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_harris(HarrisLevels lvs, const float* __restrict__ gk, float alpha) {
   constexpr int NT = HarrisShape<F>::NT, RPT = HarrisShape<F>::RPT, NPAIR = HarrisShape<F>::NPAIR;
   constexpr int TH = HarrisShape<F>::TH;
   constexpr bool PP = HarrisShape<F>::PP;
+  constexpr bool MF = HarrisShape<F>::MF;
+  static_assert(!MF || (TH == 64 && NT == 256), "MFMA form: 4 waves x 64 rows");
   // this workgroup's level (one launch may hold several pyramid levels: the small levels'
   // tiles share a launch instead of each paying a launch and a tail)
   int li = 0;
@@ -142,9 +177,10 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   // a 16-lane group of a ds_read_b128 holds 8 column groups x 2 row groups (RPT rows apart):
   // RPT * stride / 4 == 8 (mod 16) 16-B chunks keeps the chunks 8*rq + tq (mod 16) distinct,
   // i.e. stride == 8 (mod 32) floats for RPT 4 and == 16 (mod 32) for RPT 2
-  constexpr int PWP = RPT == 4 ? ((kHT + KS - 1 <= 72 && 60 + NVP <= 72) ? 72 : ((60 + NVP <= 104) ? 104 : 136))
+  constexpr int PWP = MF ? MfWin<KS>::stride()
+                    : RPT == 4 ? ((kHT + KS - 1 <= 72 && 60 + NVP <= 72) ? 72 : ((60 + NVP <= 104) ? 104 : 136))
                                : ((kHT + KS - 1 <= 80 && 60 + NVP <= 80) ? 80 : ((60 + NVP <= 112) ? 112 : 144));
-  static_assert(PWP >= kHT + KS - 1 && 60 + NVP <= PWP, "harris LDS row stride");
+  static_assert(PWP >= kHT + KS - 1 && (MF || 60 + NVP <= PWP), "harris LDS row stride");
   constexpr int NS = PWP / 4;               // 4-wide gradient strips per row
   constexpr int XA = (GA + 1 + 3) / 4 * 4;  // image tile margin left of the output tile
   constexpr int SH = XA - GA - 1;           // image column of gradient column 0, minus 1
@@ -188,6 +224,21 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     s_tp[r][p][j] = f32x2{(i0 >= 0 && i0 < KS) ? gk[i0 * KS + j] : 0.0f, (i1 >= 0 && i1 < KS) ? gk[i1 * KS + j] : 0.0f};
   }
   const int lane = tid & 63, wv = tid >> 6;
+  // MFMA window: the banded tap operand A(dy, s), lane 4b+i: g[dy][s - i] (0 off the band).
+  // Every block of an A operand holds the same taps, so the instruction's A broadcast
+  // (cbsz 4: block abid's A to all 16 blocks; tools/mfma_f32_probe.hip) lets one VGPR carry
+  // 16 steps: step k = dy * NS + s sits in block k % 16 of tapV[k / 16]
+  constexpr int MNS = MF ? MfWin<KS>::NS : 1;
+  constexpr int NTAPV = MF ? (KS * MNS + 15) / 16 : 1;
+  float tapV[NTAPV];
+  if constexpr (MF) {
+#pragma unroll
+    for (int v = 0; v < NTAPV; ++v) {
+      const int k = 16 * v + (lane >> 2), dy = k / MNS, t = k % MNS - (lane & 3);
+      const bool on = k < KS * MNS && t >= 0 && t < KS;
+      tapV[v] = on ? gk[on ? dy * KS + t : 0] : 0.0f;
+    }
+  }
   const int tq = (lane & 7) | ((wv & 1) << 3);          // columns 4tq .. 4tq+3
   const int rq = ((lane >> 3) & 7) | ((wv >> 1) << 3);  // rows RPT*rq .. RPT*rq+RPT-1
 
@@ -222,6 +273,8 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     }
   };
   if (wgx < ntiles) prefetch(wgx);
+  if (lvs.stagger && (blockIdx.x & 1))  // A/B: offset co-resident workgroups' phases
+    for (int i = 0; i < lvs.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   const int tmax = (ntiles + nwg - 1) / nwg;  // tiles of the busiest workgroup
   for (int tile = wgx; tile < ntiles; tile += nwg) {
     if (lvs.prio) {
@@ -375,6 +428,86 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
       if (tile + nwg < ntiles) prefetch(tile + nwg);
     }
 
+    if constexpr (MF) {
+      // 2'. window sums on the matrix pipe (see MfWin): lane l = tile row l, wave w = tile
+      //     columns 16w .. 16w+15 as 4 strips q of 4 columns; acc[q][pl][i] = column
+      //     16w + 4q + i.  Per tap row dy the lane reads its gradient row l + dy (columns
+      //     16w .. 16w + NC - 1), forms the three products of each column once (the same IEEE
+      //     products as :61-63) and feeds every strip whose band covers that column.
+      using MW = MfWin<KS>;
+      typedef float f32x4 __attribute__((ext_vector_type(4)));
+      f32x4 macc[4][3];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) macc[q][pl] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      // gradient rows are read one tap row ahead (two register buffers)
+      float X[2][4 * MW::NB4], Y[2][4 * MW::NB4];
+      auto load_row = [&](int dy, float (&x)[4 * MW::NB4], float (&y)[4 * MW::NB4]) {
+        const float4* rx = reinterpret_cast<const float4*>(&s_g[0][lane + dy][16 * wv]);
+        const float4* ry = reinterpret_cast<const float4*>(&s_g[1][lane + dy][16 * wv]);
+#pragma unroll
+        for (int c4 = 0; c4 < MW::NB4; ++c4) {
+          const float4 a = rx[c4], c = ry[c4];
+          x[4 * c4] = a.x, x[4 * c4 + 1] = a.y, x[4 * c4 + 2] = a.z, x[4 * c4 + 3] = a.w;
+          y[4 * c4] = c.x, y[4 * c4 + 1] = c.y, y[4 * c4 + 2] = c.z, y[4 * c4 + 3] = c.w;
+        }
+      };
+      load_row(0, X[0], Y[0]);
+      constexpr int NDY = (ABL == 2) ? 1 : KS;
+      static_for<NDY>([&](auto dyc) {
+        constexpr int dy = decltype(dyc)::value, cb = dy & 1;
+        if constexpr (dy + 1 < NDY) load_row(dy + 1, X[cb ^ 1], Y[cb ^ 1]);
+        // the row's products, once per column
+        float pxx[MW::NC], pyy[MW::NC], pxy[MW::NC];
+#pragma unroll
+        for (int c = 0; c < MW::NC; ++c) {
+          const float xv = X[cb][c], yv = Y[cb][c];
+          pxx[c] = xv * xv, pyy[c] = yv * yv, pxy[c] = xv * yv;
+        }
+        // step-major: every step feeds all 12 accumulators (4 strips x 3 planes), so an
+        // accumulator's next MFMA is 12 instructions behind its last
+        static_for<MW::NS>([&](auto sc) {
+          constexpr int s = decltype(sc)::value, k = dy * MW::NS + s;
+          const float tv = tapV[k / 16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            macc[q][0] = __builtin_amdgcn_mfma_f32_4x4x1f32(tv, pxx[4 * q + s], macc[q][0], 4, k % 16, 0);
+            macc[q][1] = __builtin_amdgcn_mfma_f32_4x4x1f32(tv, pyy[4 * q + s], macc[q][1], 4, k % 16, 0);
+            macc[q][2] = __builtin_amdgcn_mfma_f32_4x4x1f32(tv, pxy[4 * q + s], macc[q][2], 4, k % 16, 0);
+          }
+        });
+      });
+      // 3'. R (:71-74) per pixel, the digit-1 histogram, R stored as 16-B row segments
+      const int gy = ty0 + lane;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gx0 = tx0 + 16 * wv + 4 * q;
+        float Rq[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float sxx = macc[q][0][i], syy = macc[q][1][i], sxy = macc[q][2][i];
+          const float t1v = sxx * syy;
+          const float t2v = sxy * sxy;
+          const float det = t1v - t2v;
+          const float tr = sxx + syy;
+          const float tr2 = tr * tr;
+          const float at = alpha * tr2;
+          Rq[i] = det - at;
+          if (ABL != 1) atomicAdd(&s_hist[fkey(Rq[i]) >> (32 - kMedBits1)], (gy < H && gx0 + i < W) ? 1u : 0u);
+        }
+        if (gy < H) {
+          float* dst = Rp + (int64_t)gy * W + gx0;
+          if (VEC) {
+            if (gx0 < W) *reinterpret_cast<float4*>(dst) = make_float4(Rq[0], Rq[1], Rq[2], Rq[3]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (gx0 + i < W) dst[i] = Rq[i];
+          }
+        }
+      }
+    } else {
     // 2. window sums (:67-69): per pixel an fma chain over the KS x KS taps in row-major
     //    order.  acc[p][pl][q] = (row 4rq+2p, row 4rq+2p+1) at column 4tq+q; gradient row
     //    4rq+r feeds tap row r-2p of the pair's first row and r-2p-1 of its second: packed
@@ -484,6 +617,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
         }
       }
     }
+    }  // !MF
     if constexpr (ABL == 3) {
       if (tid == 0 && stamp && nst < kStampSlots - 4) stamp[4 + nst] = wall_clock64();
       ++nst;
@@ -577,10 +711,17 @@ static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipSt
   // workgroup (over the batch) take the 64 x 32 form (0: never)
   static const int small = env_int("SFMFEAT_HARRIS_SMALL", kHarrisSmallTiles);
   g.prio = prio;
+  // SFMFEAT_HARRIS_STAGGER=n: odd workgroups sleep n x 8k cycles before their first tile (A/B)
+  static const int stagger = env_int("SFMFEAT_HARRIS_STAGGER", 0);
+  g.stagger = stagger;
   // SFMFEAT_HARRIS_PP=1: product planes in LDS (form 3) instead of gradient planes (A/B)
   static const int pp = env_int("SFMFEAT_HARRIS_PP", kHarrisProductPlanes);
+  // SFMFEAT_HARRIS_MF=1: window sums on the matrix pipe (form 4) for the levels that take
+  // form 0; 2: for every level
+  static const int mf = env_int("SFMFEAT_HARRIS_MF", kHarrisMfma);
   if constexpr (KS == 7) {  // the alternative forms are built for the 7 x 7 window only
     if (npair == 1) return launch_form<KS, ABL, 1>(g, B, gk, alpha, st);
+    if (mf == 2) return launch_form<KS, ABL, 4>(g, B, gk, alpha, st);
     bool sm = small > 0;
     for (int k = 0; k < g.n; ++k) {
       const int64_t t64 = (int64_t)((g.l[k].W + kHT - 1) / kHT) * ((g.l[k].H + kHT - 1) / kHT) * B;
@@ -588,6 +729,7 @@ static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipSt
     }
     if (sm) return launch_form<KS, ABL, 2>(g, B, gk, alpha, st);
     if (pp == 1) return launch_form<KS, ABL, 3>(g, B, gk, alpha, st);
+    if (mf == 1) return launch_form<KS, ABL, 4>(g, B, gk, alpha, st);
   }
   launch_form<KS, ABL, 0>(g, B, gk, alpha, st);
 }

@@ -211,6 +211,7 @@ struct HarrisLevels {
   } l[kHarrisMaxLevels];
   int n;
   int prio;  // 1: waves raise their issue priority with the tiles they have left (A/B)
+  int stagger;  // n > 0: odd workgroups sleep n x 8k cycles before their first tile (A/B)
 };
 void launch_harris_levels(const HarrisLevels& g, int B, const float* d_gauss, int ks, float alpha,
                           hipStream_t st);
