@@ -112,11 +112,17 @@ __device__ int64_t g_harris_stamps_cap;  // u64 slots behind g_harris_stamps (wo
 //   4: the window sums on the matrix pipe (v_mfma_f32_4x4x1_16b_f32, see "MFMA window"
 //      below): 256 threads, 64 x 64 tiles, 2 workgroups per CU; wave w owns tile columns
 //      16w .. 16w+15 and lane l tile row l.
+//   5: as 0, with S_xy on the matrix pipe beside the VALU's S_xx and S_yy: the lanes of each
+//      4-lane MFMA block share their 4 columns and hold 4 different row groups (rq from lane
+//      bits 0-1 and 5, tq from bits 2-4), so an MFMA accumulator per output row o puts
+//      pixel (4rq + o, 4tq + i) in register i of the thread that owns it in form 0, and the
+//      B operand is the IxIy product that thread already formed for its VALU work.
 template <int F>
 struct HarrisShape {
   static constexpr bool PP = F == 3;                     // product planes in LDS
   static constexpr bool MF = F == 4;                     // window sums on MFMA
-  static constexpr int NPAIR = (F == 0 || F == 3 || F == 4) ? 2 : 1;  // output row pairs per thread
+  static constexpr bool HY = F == 5;                     // S_xy on MFMA, S_xx / S_yy on VALU
+  static constexpr int NPAIR = (F == 0 || F == 3 || F == 4 || F == 5) ? 2 : 1;  // output row pairs per thread
   static constexpr int NT = F == 1 ? 512 : 256;          // threads per workgroup
   static constexpr int RPT = 2 * NPAIR;                  // output rows per thread
   static constexpr int TH = RPT * 4 * (NT / 64);         // tile rows (tile columns: kHT)
@@ -156,6 +162,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   constexpr int TH = HarrisShape<F>::TH;
   constexpr bool PP = HarrisShape<F>::PP;
   constexpr bool MF = HarrisShape<F>::MF;
+  constexpr bool HY = HarrisShape<F>::HY;
   static_assert(!MF || (TH == 64 && NT == 256), "MFMA form: 4 waves x 64 rows");
   // this workgroup's level (one launch may hold several pyramid levels: the small levels'
   // tiles share a launch instead of each paying a launch and a tail)
@@ -178,6 +185,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   // RPT * stride / 4 == 8 (mod 16) 16-B chunks keeps the chunks 8*rq + tq (mod 16) distinct,
   // i.e. stride == 8 (mod 32) floats for RPT 4 and == 16 (mod 32) for RPT 2
   constexpr int PWP = MF ? MfWin<KS>::stride()
+                    : HY ? ((kHT + KS - 1 <= 76 && 60 + NVP <= 76) ? 76 : ((60 + NVP <= 108) ? 108 : 140))
                     : RPT == 4 ? ((kHT + KS - 1 <= 72 && 60 + NVP <= 72) ? 72 : ((60 + NVP <= 104) ? 104 : 136))
                                : ((kHT + KS - 1 <= 80 && 60 + NVP <= 80) ? 80 : ((60 + NVP <= 112) ? 112 : 144));
   static_assert(PWP >= kHT + KS - 1 && (MF || 60 + NVP <= PWP), "harris LDS row stride");
@@ -228,10 +236,10 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   // Every block of an A operand holds the same taps, so the instruction's A broadcast
   // (cbsz 4: block abid's A to all 16 blocks; tools/mfma_f32_probe.hip) lets one VGPR carry
   // 16 steps: step k = dy * NS + s sits in block k % 16 of tapV[k / 16]
-  constexpr int MNS = MF ? MfWin<KS>::NS : 1;
-  constexpr int NTAPV = MF ? (KS * MNS + 15) / 16 : 1;
+  constexpr int MNS = (MF || HY) ? MfWin<KS>::NS : 1;
+  constexpr int NTAPV = (MF || HY) ? (KS * MNS + 15) / 16 : 1;
   float tapV[NTAPV];
-  if constexpr (MF) {
+  if constexpr (MF || HY) {
 #pragma unroll
     for (int v = 0; v < NTAPV; ++v) {
       const int k = 16 * v + (lane >> 2), dy = k / MNS, t = k % MNS - (lane & 3);
@@ -239,8 +247,10 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
       tapV[v] = on ? gk[on ? dy * KS + t : 0] : 0.0f;
     }
   }
-  const int tq = (lane & 7) | ((wv & 1) << 3);          // columns 4tq .. 4tq+3
-  const int rq = ((lane >> 3) & 7) | ((wv >> 1) << 3);  // rows RPT*rq .. RPT*rq+RPT-1
+  // columns 4tq .. 4tq+3, rows RPT*rq .. RPT*rq+RPT-1 (HY: a 4-lane block shares tq)
+  const int tq = HY ? (((lane >> 2) & 7) | ((wv & 1) << 3)) : ((lane & 7) | ((wv & 1) << 3));
+  const int rq = HY ? ((lane & 3) | (((lane >> 5) & 1) << 2) | ((wv >> 1) << 3))
+                    : (((lane >> 3) & 7) | ((wv >> 1) << 3));
 
   // image tile of `tile` -> registers (zero outside the image = BORDER_CONSTANT)
   typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -519,6 +529,11 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
       for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc[p][pl][q] = f32x2{0.0f, 0.0f};
+    // HY: S_xy of output row RPT*rq + o in MFMA accumulator o (register i = column 4tq + i)
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    f32x4 macc2[HY ? 4 : 1];
+#pragma unroll
+    for (int o = 0; o < (HY ? 4 : 1); ++o) macc2[o] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     constexpr int NR = (ABL == 2) ? 1 : KS + 2 * NPAIR - 1;  // gradient rows feeding this thread
     static_for<NR>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
@@ -569,7 +584,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
         const bool v1 = i1 >= 0 && i1 < KS && ABL != 2;
         if (!v0 && !v1) continue;  // (a compile-time condition)
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
+        for (int pl = 0; pl < (HY ? 2 : 3); ++pl)
 #pragma unroll
           for (int j = 0; j < KS; ++j)
 #pragma unroll
@@ -585,6 +600,19 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
               }
             }
       }
+      if constexpr (HY) {
+        // S_xy: gradient row r is tap row r - o of output row o; step s takes column 4tq + s
+        // (the thread's own IxIy product) with the banded taps (MfWin)
+        static_for<RPT>([&](auto oc) {
+          constexpr int o = decltype(oc)::value, dy = r - o;
+          if constexpr (dy >= 0 && dy < KS && (ABL != 2 || dy == 0)) {
+            static_for<MNS>([&](auto sc) {
+              constexpr int st = decltype(sc)::value, k = dy * MNS + st;
+              macc2[o] = __builtin_amdgcn_mfma_f32_4x4x1f32(tapV[k / 16], P[2][st >> 1][st & 1], macc2[o], 4, k % 16, 0);
+            });
+          }
+        });
+      }
     });
     // 3. R = det - alpha * trace^2 (:71-74), digit-1 histogram of R, R stored as 16-B
     //    row segments (a wave writes 8 rows x 128 contiguous bytes per store)
@@ -596,7 +624,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float sxx = acc[o >> 1][0][q][o & 1], syy = acc[o >> 1][1][q][o & 1],
-                    sxy = acc[o >> 1][2][q][o & 1];
+                    sxy = HY ? macc2[HY ? o : 0][q] : acc[o >> 1][2][q][o & 1];
         const float t1v = sxx * syy;
         const float t2v = sxy * sxy;
         const float det = t1v - t2v;
@@ -717,11 +745,13 @@ static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipSt
   // SFMFEAT_HARRIS_PP=1: product planes in LDS (form 3) instead of gradient planes (A/B)
   static const int pp = env_int("SFMFEAT_HARRIS_PP", kHarrisProductPlanes);
   // SFMFEAT_HARRIS_MF=1: window sums on the matrix pipe (form 4) for the levels that take
-  // form 0; 2: for every level
+  // form 0; 2: for every level; 3 / 4: S_xy on MFMA beside the VALU (form 5), form-0 levels
+  // / every level
   static const int mf = env_int("SFMFEAT_HARRIS_MF", kHarrisMfma);
   if constexpr (KS == 7) {  // the alternative forms are built for the 7 x 7 window only
     if (npair == 1) return launch_form<KS, ABL, 1>(g, B, gk, alpha, st);
     if (mf == 2) return launch_form<KS, ABL, 4>(g, B, gk, alpha, st);
+    if (mf == 4) return launch_form<KS, ABL, 5>(g, B, gk, alpha, st);
     bool sm = small > 0;
     for (int k = 0; k < g.n; ++k) {
       const int64_t t64 = (int64_t)((g.l[k].W + kHT - 1) / kHT) * ((g.l[k].H + kHT - 1) / kHT) * B;
@@ -730,6 +760,7 @@ static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipSt
     if (sm) return launch_form<KS, ABL, 2>(g, B, gk, alpha, st);
     if (pp == 1) return launch_form<KS, ABL, 3>(g, B, gk, alpha, st);
     if (mf == 1) return launch_form<KS, ABL, 4>(g, B, gk, alpha, st);
+    if (mf == 3) return launch_form<KS, ABL, 5>(g, B, gk, alpha, st);
   }
   launch_form<KS, ABL, 0>(g, B, gk, alpha, st);
 }

@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <type_traits>
+#include <utility>
 #include <vector>
 
 #define CK(x)                                                                           \
@@ -103,6 +104,91 @@ __global__ void __launch_bounds__(512) k_coissue(float* out, long long* cyc, int
   }
   const long long t1 = __builtin_amdgcn_s_memtime();
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  if (l == 0) cyc[blockIdx.x * 8 + w] = t1 - t0;
+}
+
+template <int... I, class F>
+__device__ __forceinline__ void sfor_impl(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+// 5. the Harris window's inner loop in isolation: per "row" 22 columns, 4 strips x 3 planes
+// x 10 steps = 120 MFMAs on 12 accumulators.  V: 0 = MFMA only (B constant), 1 = + cbsz/abid
+// tap broadcast, 2 = + v_mul products per column (registers), 3 = + LDS row reads (b128)
+template <int V, int PARTNER = 0>
+__global__ void __launch_bounds__(512) k_win(float* out, long long* cyc, int rows) {
+  __shared__ float s_g[2][72][76];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 2 * 72 * 76; i += blockDim.x) (&s_g[0][0][0])[i] = 1.0f + 1e-3f * (i % 97);
+  __syncthreads();
+  if (w >= 4) {  // partner waves: scalar v_fma_f32 chains (PARTNER iterations of 16 fmas)
+    float a[16];
+    for (int i = 0; i < 16; ++i) a[i] = 1e-3f * (i + l);
+    const long long t0 = __builtin_amdgcn_s_memtime();
+    for (int r = 0; r < PARTNER; ++r)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) a[i] = __builtin_fmaf(a[i], 0.999f, 1e-4f);
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    float sum = 0.f;
+    for (int i = 0; i < 16; ++i) sum += a[i];
+    out[blockIdx.x * 512 + threadIdx.x] = sum;
+    if (l == 0) cyc[blockIdx.x * 8 + w] = t1 - t0;
+    return;
+  }
+  float tapV[5];
+  for (int v = 0; v < 5; ++v) tapV[v] = 0.01f * (v + 1) + 1e-4f * l;
+  f32x4 acc[4][3];
+  for (int q = 0; q < 4; ++q)
+    for (int p = 0; p < 3; ++p) acc[q][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float X[24], Y[24];
+  for (int c = 0; c < 24; ++c) X[c] = 1.0f + c * 1e-3f + l * 1e-5f, Y[c] = 0.5f + c * 1e-3f;
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  for (int r = 0; r < rows; ++r) {
+    if constexpr (V >= 3) {
+      const float4* rx = reinterpret_cast<const float4*>(&s_g[0][(l + r) % 8 + l][16 * w]);
+      const float4* ry = reinterpret_cast<const float4*>(&s_g[1][(l + r) % 8 + l][16 * w]);
+#pragma unroll
+      for (int c4 = 0; c4 < 6; ++c4) {
+        const float4 a = rx[c4], b = ry[c4];
+        X[4 * c4] = a.x, X[4 * c4 + 1] = a.y, X[4 * c4 + 2] = a.z, X[4 * c4 + 3] = a.w;
+        Y[4 * c4] = b.x, Y[4 * c4 + 1] = b.y, Y[4 * c4 + 2] = b.z, Y[4 * c4 + 3] = b.w;
+      }
+    }
+    float pxx[22], pyy[22], pxy[22];
+#pragma unroll
+    for (int c = 0; c < 22; ++c) {
+      if constexpr (V >= 2) pxx[c] = X[c] * X[c], pyy[c] = Y[c] * Y[c], pxy[c] = X[c] * Y[c];
+      else pxx[c] = X[c], pyy[c] = Y[c], pxy[c] = X[0];
+    }
+    sfor<10>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (V >= 1) {
+          acc[q][0] = __builtin_amdgcn_mfma_f32_4x4x1f32(tapV[s / 4], pxx[4 * q + s], acc[q][0], 4, s % 4, 0);
+          acc[q][1] = __builtin_amdgcn_mfma_f32_4x4x1f32(tapV[s / 4], pyy[4 * q + s], acc[q][1], 4, s % 4, 0);
+          acc[q][2] = __builtin_amdgcn_mfma_f32_4x4x1f32(tapV[s / 4], pxy[4 * q + s], acc[q][2], 4, s % 4, 0);
+        } else {
+          acc[q][0] = __builtin_amdgcn_mfma_f32_4x4x1f32(tapV[s / 4], pxx[4 * q + s], acc[q][0], 0, 0, 0);
+          acc[q][1] = __builtin_amdgcn_mfma_f32_4x4x1f32(tapV[s / 4], pyy[4 * q + s], acc[q][1], 0, 0, 0);
+          acc[q][2] = __builtin_amdgcn_mfma_f32_4x4x1f32(tapV[s / 4], pxy[4 * q + s], acc[q][2], 0, 0, 0);
+        }
+      }
+    });
+    if constexpr (V < 3) {  // keep the row data live and changing without memory
+#pragma unroll
+      for (int c = 0; c < 24; ++c) X[c] = __builtin_amdgcn_fmed3f(X[c], Y[c], 2.0f);
+    }
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  float sum = 0.f;
+  for (int q = 0; q < 4; ++q)
+    for (int p = 0; p < 3; ++p) sum += acc[q][p][0] + acc[q][p][3];
+  out[blockIdx.x * 512 + threadIdx.x] = sum;
   if (l == 0) cyc[blockIdx.x * 8 + w] = t1 - t0;
 }
 
@@ -276,5 +362,38 @@ int main() {
     printf("4. co-issue %s: MFMA waves %.0f ticks (%d x 8 MFMA), VALU waves %.0f ticks (%d x 8 v_pk_fma_f32)\n",
            mode == 0 ? "MFMA alone" : mode == 1 ? "VALU alone" : "both      ", sm / 1024, imm, sv / 1024, ivv);
   }
+  // 5. window loop in isolation: (a) 2 workgroups of 4 MFMA waves per CU (2 MFMA waves per
+  // SIMD), (b) 1 per CU (1 MFMA wave per SIMD), (c) 1 per CU + 4 scalar-VALU partner waves
+  CK(hipMalloc(&dout, 1024 * 512 * 4));
+  CK(hipFree(dcyc));
+  CK(hipMalloc(&dcyc, 1024 * 8 * 8));
+  cyc.resize(1024 * 8);
+  auto win = [&](const char* name, auto kern, int blocks, int threads, int rows) {
+    CK(hipEventRecord(e0));
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, 0, dout, dcyc, rows);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipMemcpy(cyc.data(), dcyc, blocks * 8 * 8, hipMemcpyDeviceToHost));
+    double sc = 0, sp = 0;
+    int np = 0;
+    for (int b = 0; b < blocks; ++b)
+      for (int w = 0; w < 8; ++w) {
+        if (w < 4) sc += (double)cyc[b * 8 + w];
+        else if (threads > 256) sp += (double)cyc[b * 8 + w], ++np;
+      }
+    const double mf = (double)rows * 120;
+    const double per_simd = mf * blocks * 4 / 1024;
+    printf("5. %-44s %.3f ms, %.2f ticks per MFMA per MFMA wave, %.2f ns per MFMA per SIMD; partner %.0f ticks\n", name, ms,
+           sc / (blocks * 4) / mf, ms * 1e6 / per_simd, np ? sp / np : 0.0);
+  };
+  win("V=0 MFMA only, 2 MFMA waves/SIMD", k_win<0>, 512, 256, 512);
+  win("V=3 LDS+products, 2 MFMA waves/SIMD", k_win<3>, 512, 256, 512);
+  win("V=0 MFMA only, 1 MFMA wave/SIMD", k_win<0>, 256, 256, 1024);
+  win("V=3 LDS+products, 1 MFMA wave/SIMD", k_win<3>, 256, 256, 1024);
+  win("V=3, 1 MFMA wave/SIMD + idle partner", k_win<3, 0>, 256, 512, 1024);
+  win("V=3, 1 MFMA wave/SIMD + scalar-fma partner", k_win<3, 4096>, 256, 512, 1024);
+  win("partner alone (V=3 rows 0)", k_win<3, 4096>, 256, 512, 0);
   return bad ? 1 : 0;
 }
