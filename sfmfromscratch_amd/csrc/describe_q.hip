@@ -21,6 +21,9 @@
 #include "kernels.h"
 
 #include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
 
 namespace sfm {
 namespace dq {
@@ -62,6 +65,14 @@ SFM_DEV uint32_t edge_key(double e, double sh, bool strict) {
   for (int it = 0; it < 64 && !pass(kc); ++it) ++kc;
   return kc;
 }
+
+// Bin-edge keys, the same for every keypoint, computed once per device by the host (the same
+// IEEE double arithmetic as pi_edge / edge_key above, fp-contract off on both sides):
+// c_ori[j] = edge_key(linspace(-pi, pi, 37)[j], 0, j == 36) (orientation histogram) and
+// c_cell[bi][t] = edge_key(linspace(-pi, pi, 9)[t], dom_bi, t == 8) with dom_bi the centre of
+// orientation bin bi (bi < 36), dom = 0 in row 36 (the non-rotated NaiveSIFT path).
+__constant__ uint32_t c_ori[37];
+__constant__ uint32_t c_cell[37][9];
 
 // ---- row-local (16-lane) exchanges --------------------------------------------------
 template <int CTRL>
@@ -281,6 +292,7 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
   __syncthreads();
 
   double dom = 0.0;
+  int dom_bin = 36;  // row of c_cell (36: dom = 0)
   if constexpr (ROT) {
     // 3. dominant orientation (ScaleRotInvSIFT.py:24-31): np.histogram's cumulative path
     if constexpr ((ABL & 1) == 0) merge_level<E, 2>(k, gl);
@@ -347,7 +359,7 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
       if ((ABL & 16) != 0 && j <= 36) {
         sI[j] = j * N / 37;
       } else if (j <= 36) {
-        const uint32_t T = edge_key(pi_edge(j, 37), 0.0, j == 36);
+        const uint32_t T = c_ori[j];
         int lo = 0;
         constexpr int S0 = pow2ceil(N + 1) / 2;
 #pragma unroll
@@ -383,10 +395,11 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
       if (ov > hb || (ov == hb && oi < bi)) { hb = ov; bi = oi; }
     }
     dom = (pi_edge(bi, 37) + pi_edge(bi + 1, 37)) / 2.0;
+    dom_bin = bi;
   }
 
   // 4. the 4 x 4 cells of 4 x 4 px from the window's top-left (:68-76), 8 bins each
-  if (gl < 9) sT[gl] = (ABL & 32) ? 0x80000000u + (uint32_t)(dom * 1e6) * gl : edge_key(pi_edge(gl, 9), dom, gl == 8);
+  if (gl < 9) sT[gl] = (ABL & 32) ? 0x80000000u + (uint32_t)(dom * 1e6) * gl : c_cell[dom_bin][gl];
   __syncthreads();  // (also: the rotate prefix sums in sA are no longer read)
   float hv[8];
   if constexpr ((ABL & 4) != 0) {
@@ -537,6 +550,54 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
 }
 
 }  // namespace dq
+
+namespace {
+uint32_t fkey_h(float v) {
+  uint32_t b;
+  memcpy(&b, &v, 4);
+  if (b == 0x80000000u) b = 0u;
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+float fkey_inv_h(uint32_t k) {
+  const uint32_t b = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  float f;
+  memcpy(&f, &b, 4);
+  return f;
+}
+double pi_edge_h(int i, int num) {  // = dq::pi_edge
+  const double start = -3.141592653589793, stop = 3.141592653589793;
+  if (i == num - 1) return stop;
+  const double step = (stop - start) / (double)(num - 1);
+  return (double)i * step + start;
+}
+uint32_t edge_key_h(double e, double sh, bool strict) {  // = dq::edge_key
+  uint32_t kc = fkey_h((float)(e + sh));
+  auto pass = [&](uint32_t kk) {
+    const double d = (double)fkey_inv_h(kk) - sh;
+    return strict ? d > e : d >= e;
+  };
+  for (int it = 0; it < 64 && pass(kc); ++it) --kc;
+  for (int it = 0; it < 64 && !pass(kc); ++it) ++kc;
+  return kc;
+}
+}  // namespace
+
+void init_describe_quad_tables() {
+  static std::mutex mu;
+  static bool done[256] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 256) return;
+  std::lock_guard<std::mutex> lk(mu);
+  if (done[dev]) return;
+  uint32_t ori[37], cell[37][9];
+  for (int j = 0; j < 37; ++j) ori[j] = edge_key_h(pi_edge_h(j, 37), 0.0, j == 36);
+  for (int bi = 0; bi < 37; ++bi) {
+    const double dom = bi < 36 ? (pi_edge_h(bi, 37) + pi_edge_h(bi + 1, 37)) / 2.0 : 0.0;
+    for (int t = 0; t < 9; ++t) cell[bi][t] = edge_key_h(pi_edge_h(t, 9), dom, t == 8);
+  }
+  done[dev] = hipMemcpyToSymbol(HIP_SYMBOL(dq::c_ori), ori, sizeof(ori)) == hipSuccess &&
+              hipMemcpyToSymbol(HIP_SYMBOL(dq::c_cell), cell, sizeof(cell)) == hipSuccess;
+}
 
 #define SFM_DQ_BODY(WS)                                                                              \
     if (rotate)                                                                                      \

@@ -243,6 +243,8 @@ void launch_nms(const float* R, const MedianState* state, uint64_t* cand,
 // predicate into cand (n u64 per plane), then the same top-k.  scratch: n u64 per plane.
 void init_topk_attributes();
 void init_describe_attributes(size_t max_lds);
+// the quad describe kernel's bin-edge key tables on the current device (once per device)
+void init_describe_quad_tables();
 size_t describe_lds_bytes(int fw, int rotate);
 void launch_select(const float* R, uint64_t* cand, const unsigned long long* cand_count, uint32_t* medlist,
                    uint64_t* scratch, KpList kp, int kcap, int k, int B, int H, int W, int ksize, int half_window,

@@ -91,7 +91,9 @@ struct sfm_ctx {
   int last_H = 0, last_W = 0;
   // stage profiling (sfm_profile_*): HIP events bracketing each stage's launches
   bool prof = false;
-  uint32_t prof_mask = ~0u;  // stages bracketed while profiling (sfm_profile_stages)
+  uint32_t prof_mask = ~0u;
+  int64_t extractions = 0;  // extract_impl calls (SFMFEAT_SKIP leaves the first one whole)
+  int64_t match_calls = 0;  // match sub-launches (likewise)  // stages bracketed while profiling (sfm_profile_stages)
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
   std::vector<hipEvent_t> prof_pool;
   double prof_ms[SFM_PROF_STAGES] = {0};
@@ -258,6 +260,18 @@ int reserve_impl(sfm_ctx* c, int B, int H, int W) {
   return SFM_OK;
 }
 
+// SFMFEAT_SKIP=mask (timing bounds only, results wrong by design): stages whose launches are
+// left out from a context's second extraction on (the first fills every buffer the skipped
+// stages' consumers read) — 1 keypoint selection, 2 descriptors, 8 match sweep + re-rank,
+// 16 Harris of the levels above 0
+int skip_mask() {
+  static const int m = [] {
+    const char* e = getenv("SFMFEAT_SKIP");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
+
 int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy, float* desc,
                  float* conf, int32_t* count, int64_t cap, hipStream_t st) {
   if (B < 1 || H < 1 || W < 1) return set_err(c, SFM_EINVAL, "empty batch or image");
@@ -268,6 +282,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   int rc = reserve_impl(c, B, H, W);
   if (rc) return rc;
   const int L = c->L;
+  const int skip = c->extractions++ > 0 ? skip_mask() : 0;
   if (c->gate && c->gate->armed) HIPCHK(c, hipStreamWaitEvent(st, c->gate->ev, 0));
   c->last_B = B;
   c->last_H = H;
@@ -366,12 +381,14 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     // the scratch regions of this level's stream (the aux stream's levels and the caller
     // stream's levels select concurrently)
     const int64_t so = l < L_aux ? 0 : (int64_t)B * H * W;
+    if (skip & 1) return;
     launch_select(e.R, e.cand, candcnt + e.co, as<uint32_t>(c->d_medlist) + so, as<uint64_t>(c->d_scratch) + so, e.kp,
                   std::max(c->kcap, 1), c->kcap, B, lv[l].h, lv[l].w, c->p.ksize, lv[l].fw / 2, e.med, s);
   };
   bool counted = false;  // the last level's describe launch wrote the slot counts
   auto describe_level = [&](int l, hipStream_t s) {
     StageScope sc(c, SFM_PROF_DESCRIBE, s);
+    if ((skip & 2) && l != L - 1) return;
     const bool r = launch_describe(lvl[l], B, lv[l].h, lv[l].w, lv[l].fw, rotate, lb[l].kp, c->kcap,
                                    as<int32_t>(c->d_lc), l, L, lv[l].scale, xy, desc, conf, cap,
                                    l == L - 1 ? count : nullptr, s);
@@ -417,7 +434,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
         q.W = lv[l].w;
         q.scan = SelectScan{e.med, medcnt + e.co, donecnt + e.co, vmin, e.exact ? 1 : 0};
       }
-      launch_harris_levels(g, B, as<float>(c->d_gauss), c->p.gaussian_size, alpha, st);
+      if (!(l0 > 0 && (skip & 16))) launch_harris_levels(g, B, as<float>(c->d_gauss), c->p.gaussian_size, alpha, st);
     }
     if (gate_level >= l0 && gate_level < l1 && (rc = release_gate())) return rc;
     for (int l = l0; l < l1; ++l) {
@@ -462,7 +479,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
                                            lv[l].fw / 2};
       so += (int64_t)B * lv[l].h * lv[l].w;
     }
-    launch_select_levels(g, std::max(c->kcap, 1), c->kcap, B, c->p.ksize, st);
+    if (!(skip & 1)) launch_select_levels(g, std::max(c->kcap, 1), c->kcap, B, c->p.ksize, st);
   } else {
     for (int l = L_aux; l < L; ++l) select_level(l, st);
   }
@@ -548,7 +565,7 @@ int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, in
     if ((rc = ensure(c, c->m_candn, (size_t)Pmax * cap * 4))) return rc;
     if ((rc = ensure(c, c->m_candt, (size_t)Pmax * cap * 4))) return rc;
   }
-  for (int p0 = 0; p0 < P; p0 += Pmax) {
+  for (int p0 = 0; p0 < P; p0 += Pmax, ++c->match_calls) {
     const int Pn = std::min(Pmax, P - p0);
     const int32_t* pr = pairs + 2 * (int64_t)p0;
     if (c->match_direct) {
@@ -558,7 +575,7 @@ int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, in
     } else {
       const int64_t capP = (cap + 127) / 128 * 128;
       StageScope sc(c, SFM_PROF_MATCH, st);
-      launch_match_mfma(desc, count, cap, capP, as<_Float16>(c->m_hi), as<_Float16>(c->m_lo), as<float>(c->m_norm2),
+      if (!(c->match_calls > 0 && (skip_mask() & 8))) launch_match_mfma(desc, count, cap, capP, as<_Float16>(c->m_hi), as<_Float16>(c->m_lo), as<float>(c->m_norm2),
                         as<float>(c->m_rnorm), c->m_imgmax.p, pr, Pn, ratio, as<RowBest>(c->m_rows),
                         (int)cap, as<uint32_t>(c->m_cand), as<int32_t>(c->m_candn), as<float>(c->m_candt),
                         as<int>(c->m_ovfc), as<int2>(c->m_ovf), st);
@@ -681,6 +698,7 @@ int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out) {
   }
   init_topk_attributes();
   init_describe_attributes(describe_lds_bytes(SFM_MAX_FW, 1));
+  init_describe_quad_tables();
   init_match_attributes(kMaxMatchRows);
   *out = c;
   return SFM_OK;
