@@ -22,7 +22,7 @@ constexpr int kMedBits1 = 11;               // median digit 1 (histogrammed insi
 constexpr int kMedBins1 = 1 << kMedBits1;   // 2048 (digits 2 / 3 are 11 / 10 bits)
 constexpr int kTopkLdsCap = 8192;           // max keys sorted in LDS by the top-k kernel
 constexpr int kMaxMatchRows = 16384;        // max keypoints per image for the matcher sort
-constexpr int kMatchCandCap = 128;          // admitted targets per query row (MFMA matcher lists)
+constexpr int kMatchCandCap = 256;          // admitted targets per query row (MFMA matcher lists)
 constexpr int kCounterStride = 32;          // u64 per per-plane atomic counter (own 256-B line)
 
 // Per-plane state of the keypoint selection (NaiveSIFT.py:90-120).

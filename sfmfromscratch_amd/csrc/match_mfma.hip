@@ -589,17 +589,19 @@ __global__ void __launch_bounds__(256) k_match_rerank(const float* __restrict__ 
 #pragma unroll
   for (int i = 0; i < 16; ++i) a[i] = A[8 * i + l8];
   int nk = 0;  // window members, compacted into sJ[wv] in list order
-  static_assert(kHalfCap == 64, "one wavefront pass per half-list");
+  static_assert(kHalfCap % 64 == 0, "whole wavefront passes per half-list");
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int ch = h ? c1 : c0;
-    if (ch == 0) continue;
-    const bool in = lane < ch;
-    const uint32_t e = in ? list[h * kHalfCap + lane] : 0u;
-    const bool keep = in && __uint_as_float(e & 0xffff0000u) <= thr;
-    const uint64_t bal = __ballot(keep);
-    if (keep) sJ[wv][nk + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(e & 0xffffu);
-    nk += __popcll(bal);
+    for (int b0 = 0; b0 < ch; b0 += 64) {
+      const int idx = b0 + lane;
+      const bool in = idx < ch;
+      const uint32_t e = in ? list[h * kHalfCap + idx] : 0u;
+      const bool keep = in && __uint_as_float(e & 0xffff0000u) <= thr;
+      const uint64_t bal = __ballot(keep);
+      if (keep) sJ[wv][nk + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)(e & 0xffffu);
+      nk += __popcll(bal);
+    }
   }
   __builtin_amdgcn_wave_barrier();
   float e1 = INFINITY, e2 = INFINITY;

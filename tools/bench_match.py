@@ -13,6 +13,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--allpairs", action="store_true", help="all B(B-1)/2 pairs instead of consecutive")
+    ap.add_argument("--4k", dest="k4", action="store_true", help="BASELINE configs[4]: 4K, 5 octaves, k 8000, 8 frames")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -20,9 +21,15 @@ def main():
     from sfmfromscratch_amd.pipeline import BatchExtractor, BatchMatcher, all_pairs, consecutive_pairs
     P_OCT = {"num_interest_points": 2500, "ksize": 3, "gaussian_size": 7, "sigma": 6, "alpha": 0.05,
              "feature_width": 18, "pyramid_level": 4, "pyramid_scale_factor": 2}
+    H, W = 1080, 1920
+    if args.k4:
+        H, W = 2160, 3840
+        P_OCT.update(num_interest_points=8000, pyramid_level=5)
+        if args.batch == 32:
+            args.batch = 8
     B = args.batch
     ex = BatchExtractor(P_OCT)
-    u8 = np.stack([synth.make_frame_u8(1080, 1920, 1234, i) for i in range(B)])
+    u8 = np.stack([synth.make_frame_u8(H, W, 1234, i) for i in range(B)])
     slots = ex.extract(torch.from_numpy(u8).cuda())
     pairs = torch.from_numpy(all_pairs(B) if args.allpairs else consecutive_pairs(B)).cuda()
     m = BatchMatcher(0.85, ctx=ex.ctx)
