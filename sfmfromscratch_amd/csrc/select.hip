@@ -16,6 +16,8 @@
 // The exact path used to be four launches per level (median collect, median final, NMS,
 // top-k) that exited at once on certified planes; a plane's exact path now runs in the
 // workgroup that found it uncertified, so a certified level costs one launch in all.
+#include <stdlib.h>
+
 #include "kernels.h"
 
 namespace sfm {
@@ -100,11 +102,53 @@ struct SelectLds {
   uint32_t* cnt;   // 2
 };
 
+// The n (<= blockDim.x) keys of s[0..n) in ascending order, by runs: each wave sorts its 64
+// keys in registers (shuffle bitonic, no LDS), the sorted runs go back to LDS, and every key's
+// final position is its place in its run plus, for each other run, the number of that run's
+// keys below it (a 64-entry binary search; the runs' searches are independent).  The keys are
+// distinct (their low half is the raster index); padding (~0) sorts after every key and is not
+// stored.  Three barriers instead of the bitonic network's ~55 stages (10 block-wide).
+SFM_DEV void run_merge_sort_u64(uint64_t* s, int n) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nruns = (n + 63) >> 6;
+  uint64_t k[1] = {tid < n ? s[tid] : ~0ull};
+  if (w < nruns) wave_bitonic_sort_u64<1>(k);
+  __syncthreads();
+  if (w < nruns) s[tid] = k[0];
+  __syncthreads();
+  uint32_t pos = (uint32_t)lane;
+  if (w < nruns && k[0] != ~0ull) {
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      if (v < nruns && v != w) {
+        const uint64_t* run = s + 64 * v;
+        int lo = 0;  // keys of run v below k: the first index whose key is not below
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1)
+          if (run[lo + step - 1] < k[0]) lo += step;
+        lo += run[lo] < k[0] && lo == 63 ? 1 : 0;
+        pos += (uint32_t)lo;
+      }
+    }
+  }
+  __syncthreads();
+  if (w < nruns && k[0] != ~0ull) s[pos] = k[0];
+  __syncthreads();
+}
+
 // The kk (>= 1) smallest of the C keys cp[0..C) into L.sel[0..kk), ascending (tp: per-plane
 // scratch for tie lists that overflow LDS).
-SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, const SelectLds& L) {
+// abl (timing ablations, results wrong by design; SFMFEAT_SELECT_ABL): 1 no final sort, 2 no
+// radix select (every key counts as below the k-th)
+SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, const SelectLds& L, int abl = 0) {
   const int tid = threadIdx.x, nt = blockDim.x;
   if (C <= kTopkDirect) {
+    if (C <= nt) {
+      for (int i = tid; i < C; i += nt) L.sel[i] = cp[i];
+      __syncthreads();
+      run_merge_sort_u64(L.sel, (int)C);
+      return;
+    }
     const int P = next_pow2((int)C);
     for (int i = tid; i < P; i += nt) L.sel[i] = (i < C) ? cp[i] : ~0ull;
     __syncthreads();
@@ -131,7 +175,7 @@ SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, co
       const int64_t i = tid + (int64_t)nt * j;
       kr[j] = i < C ? cp[i] : ~0ull;
     }
-    T = radix_select_regs(kr, C, &rank, L.h, L.scan, L.out);
+    T = (abl & 2) ? 0xffffffffu : radix_select_regs(kr, C, &rank, L.h, L.scan, L.out);
     if (tid == 0) {
       L.cnt[0] = 0u;
       L.cnt[1] = 0u;
@@ -150,15 +194,19 @@ SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, co
     for (int64_t i = tid; i < C; i += nt) part(cp[i]);
   }
   __syncthreads();
-  const uint32_t nless = L.cnt[0];
+  const uint32_t nless = (abl & 2) ? min(L.cnt[0], (uint32_t)kk) : L.cnt[0];
   const uint32_t ntie = L.cnt[1];
-  const uint32_t need = rank + 1;  // ties taken, by ascending raster index
+  const uint32_t need = (abl & 2) ? 0u : rank + 1;  // ties taken, by ascending raster index
   if (ntie <= (uint32_t)kTieLdsCap) {
-    const int P = next_pow2((int)ntie);
-    for (int i = tid; i < P; i += nt)
-      if (i >= (int)ntie) L.tie[i] = ~0ull;
-    __syncthreads();
-    bitonic_sort_u64(L.tie, P);
+    if (ntie <= (uint32_t)nt) {
+      run_merge_sort_u64(L.tie, (int)ntie);
+    } else {
+      const int P = next_pow2((int)ntie);
+      for (int i = tid; i < P; i += nt)
+        if (i >= (int)ntie) L.tie[i] = ~0ull;
+      __syncthreads();
+      bitonic_sort_u64(L.tie, P);
+    }
     for (uint32_t i = tid; i < need; i += nt) L.sel[nless + i] = L.tie[i];
   } else {
     uint32_t r2 = rank;
@@ -169,6 +217,11 @@ SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, co
     }
   }
   __syncthreads();
+  if (abl & 1) return;
+  if (kk <= nt) {
+    run_merge_sort_u64(L.sel, kk);
+    return;
+  }
   const int P = next_pow2(kk);
   for (int i = tid; i < P; i += nt)
     if (i >= kk) L.sel[i] = ~0ull;
@@ -375,7 +428,7 @@ SFM_DEV int64_t exact_nms(const float* Rp, int H, int W, int kh, float med, uint
   return C;
 }
 
-__global__ void __launch_bounds__(1024) k_select(SelectLevels g, int kcap, int k, int kh, int B) {
+__global__ void __launch_bounds__(1024) k_select(SelectLevels g, int kcap, int k, int kh, int B, int abl) {
   // this workgroup's level and plane (levels are B workgroups each, level-major)
   const int li = (int)blockIdx.x / B;
   const SelectLevels::Level& lv = g.l[li];
@@ -411,8 +464,8 @@ __global__ void __launch_bounds__(1024) k_select(SelectLevels g, int kcap, int k
   if (!s.fallback) {
     const int64_t C = (int64_t)cand_count[(int64_t)b * kCounterStride];  // certified NMS's candidates
     if (C >= (int64_t)k) {
-      topk_sorted(cp, C, k, tp, L);
-      if (~(uint32_t)(L.sel[k - 1] >> 32) >= s.tcert) {  // k-th candidate above the median's bucket
+      topk_sorted(cp, C, k, tp, L, abl);
+      if ((abl & 3) || ~(uint32_t)(L.sel[k - 1] >> 32) >= s.tcert) {  // k-th candidate above the median's bucket
         emit_keypoints(L, k, kp, b, kcap, H, W, hw);
         return;
       }
@@ -438,7 +491,11 @@ size_t topk_lds_bytes() {
 
 void launch_select_levels(const SelectLevels& g, int kcap, int k, int B, int ksize, hipStream_t st) {
   if (g.n < 1 || g.n > kSelectMaxLevels || B < 1) return;
-  hipLaunchKernelGGL(k_select, dim3(B * g.n), dim3(1024), topk_lds_bytes(), st, g, kcap, k, ksize / 2, B);
+  static const int abl = [] {
+    const char* e = getenv("SFMFEAT_SELECT_ABL");
+    return e ? atoi(e) : 0;
+  }();
+  hipLaunchKernelGGL(k_select, dim3(B * g.n), dim3(1024), topk_lds_bytes(), st, g, kcap, k, ksize / 2, B, abl);
 }
 
 void launch_select(const float* R, uint64_t* cand, const unsigned long long* cand_count, uint32_t* medlist,
