@@ -108,32 +108,68 @@ struct SelectLds {
 // keys below it (a 64-entry binary search; the runs' searches are independent).  The keys are
 // distinct (their low half is the raster index); padding (~0) sorts after every key and is not
 // stored.  Three barriers instead of the bitonic network's ~55 stages (10 block-wide).
+template <int E>  // keys per lane: runs of 64 E keys, n <= E * blockDim.x
 SFM_DEV void run_merge_sort_u64(uint64_t* s, int n) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int nruns = (n + 63) >> 6;
-  uint64_t k[1] = {tid < n ? s[tid] : ~0ull};
-  if (w < nruns) wave_bitonic_sort_u64<1>(k);
+  constexpr int RL = 64 * E;  // run length
+  const int nruns = (n + RL - 1) / RL;
+  uint64_t k[E];
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const int i = w * RL + lane * E + r;
+    k[r] = i < n ? s[i] : ~0ull;
+  }
+  if (w < nruns) wave_bitonic_sort_u64<E>(k);
   __syncthreads();
-  if (w < nruns) s[tid] = k[0];
+  if (w < nruns) {
+#pragma unroll
+    for (int r = 0; r < E; ++r) s[w * RL + lane * E + r] = k[r];
+  }
   __syncthreads();
-  uint32_t pos = (uint32_t)lane;
-  if (w < nruns && k[0] != ~0ull) {
+  uint32_t pos[E];
+#pragma unroll
+  for (int r = 0; r < E; ++r) pos[r] = (uint32_t)(lane * E + r);
+  if (w < nruns) {
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
       if (v < nruns && v != w) {
-        const uint64_t* run = s + 64 * v;
-        int lo = 0;  // keys of run v below k: the first index whose key is not below
+        const uint64_t* run = s + RL * v;
 #pragma unroll
-        for (int step = 32; step >= 1; step >>= 1)
-          if (run[lo + step - 1] < k[0]) lo += step;
-        lo += run[lo] < k[0] && lo == 63 ? 1 : 0;
-        pos += (uint32_t)lo;
+        for (int r = 0; r < E; ++r) {
+          int lo = 0;  // keys of run v below k[r] (RL - 1 at most, then the last entry)
+#pragma unroll
+          for (int step = RL / 2; step >= 1; step >>= 1)
+            if (run[lo + step - 1] < k[r]) lo += step;
+          lo += (lo == RL - 1 && run[lo] < k[r]) ? 1 : 0;
+          pos[r] += (uint32_t)lo;
+        }
       }
     }
   }
   __syncthreads();
-  if (w < nruns && k[0] != ~0ull) s[pos] = k[0];
+  if (w < nruns) {
+#pragma unroll
+    for (int r = 0; r < E; ++r)
+      if (k[r] != ~0ull) s[pos[r]] = k[r];
+  }
   __syncthreads();
+}
+
+// ascending sort of s[0..n) (distinct keys; padding ~0 sorts last): runs for n <= 2 blockDim.x,
+// else the LDS bitonic network over next_pow2(n) slots (s must hold them)
+SFM_DEV void sort_keys_u64(uint64_t* s, int n) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (n <= nt && nt <= 1024) {
+    run_merge_sort_u64<1>(s, n);
+  } else if (n <= 2 * nt && nt <= 1024) {
+    run_merge_sort_u64<2>(s, n);
+  } else {
+    const int P = next_pow2(n);
+    for (int i = tid; i < P; i += nt)
+      if (i >= n) s[i] = ~0ull;
+    __syncthreads();
+    bitonic_sort_u64(s, P);
+  }
 }
 
 // The kk (>= 1) smallest of the C keys cp[0..C) into L.sel[0..kk), ascending (tp: per-plane
@@ -143,16 +179,9 @@ SFM_DEV void run_merge_sort_u64(uint64_t* s, int n) {
 SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, const SelectLds& L, int abl = 0) {
   const int tid = threadIdx.x, nt = blockDim.x;
   if (C <= kTopkDirect) {
-    if (C <= nt) {
-      for (int i = tid; i < C; i += nt) L.sel[i] = cp[i];
-      __syncthreads();
-      run_merge_sort_u64(L.sel, (int)C);
-      return;
-    }
-    const int P = next_pow2((int)C);
-    for (int i = tid; i < P; i += nt) L.sel[i] = (i < C) ? cp[i] : ~0ull;
+    for (int i = tid; i < C; i += nt) L.sel[i] = cp[i];
     __syncthreads();
-    bitonic_sort_u64(L.sel, P);
+    sort_keys_u64(L.sel, (int)C);
     return;
   }
   uint32_t rank = (uint32_t)(kk - 1);
@@ -198,15 +227,7 @@ SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, co
   const uint32_t ntie = L.cnt[1];
   const uint32_t need = (abl & 2) ? 0u : rank + 1;  // ties taken, by ascending raster index
   if (ntie <= (uint32_t)kTieLdsCap) {
-    if (ntie <= (uint32_t)nt) {
-      run_merge_sort_u64(L.tie, (int)ntie);
-    } else {
-      const int P = next_pow2((int)ntie);
-      for (int i = tid; i < P; i += nt)
-        if (i >= (int)ntie) L.tie[i] = ~0ull;
-      __syncthreads();
-      bitonic_sort_u64(L.tie, P);
-    }
+    sort_keys_u64(L.tie, (int)ntie);
     for (uint32_t i = tid; i < need; i += nt) L.sel[nless + i] = L.tie[i];
   } else {
     uint32_t r2 = rank;
@@ -218,15 +239,7 @@ SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, co
   }
   __syncthreads();
   if (abl & 1) return;
-  if (kk <= nt) {
-    run_merge_sort_u64(L.sel, kk);
-    return;
-  }
-  const int P = next_pow2(kk);
-  for (int i = tid; i < P; i += nt)
-    if (i >= kk) L.sel[i] = ~0ull;
-  __syncthreads();
-  bitonic_sort_u64(L.sel, P);
+  sort_keys_u64(L.sel, kk);
 }
 
 // Edge filter with order-preserving compaction of L.sel[0..nsel) into the plane's list.
@@ -359,37 +372,35 @@ SFM_DEV int64_t exact_nms(const float* Rp, int H, int W, int kh, float med, uint
   __syncthreads();
   auto pred_of = [&](float v, float m) { return (v < med) ? (v == 0.0f) : (v == m); };
   if (kh == 1) {
-    constexpr int NCH = 4, RB = 1;
+    // RB output rows per wavefront iteration from RB + 2 image rows loaded once (every load
+    // of the iteration in flight together)
+    constexpr int NCH = 2, RB = 4;
     for (int y0 = wid * RB; y0 < H; y0 += nw * RB) {
       for (int xb = 0; xb < W; xb += 64 * NCH) {
-        float c[RB][NCH][3], e[RB][NCH][3];
+        float c[RB + 2][NCH], e[RB + 2][NCH];
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
+        for (int rr = 0; rr < RB + 2; ++rr) {
+          const int yy = y0 - 1 + rr;
+          const bool rok = yy >= 0 && yy < H;
 #pragma unroll
           for (int ch = 0; ch < NCH; ++ch) {
-            const int y = y0 + rb;
             const int x = xb + 64 * ch + lane;
             const int xe = lane == 0 ? x - 1 : x + 1;  // edge lanes: the column beyond the chunk
-#pragma unroll
-            for (int dy = 0; dy < 3; ++dy) {
-              const int yy = y + dy - 1;
-              const bool rok = yy >= 0 && yy < H && y < H;
-              c[rb][ch][dy] = (rok && x < W) ? Rp[(int64_t)yy * W + x] : -INFINITY;
-              e[rb][ch][dy] =
-                  (rok && (lane == 0 || lane == 63) && xe >= 0 && xe < W) ? Rp[(int64_t)yy * W + xe] : -INFINITY;
-            }
+            c[rr][ch] = (rok && x < W) ? Rp[(int64_t)yy * W + x] : -INFINITY;
+            e[rr][ch] = (rok && (lane == 0 || lane == 63) && xe >= 0 && xe < W) ? Rp[(int64_t)yy * W + xe] : -INFINITY;
           }
+        }
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
           for (int ch = 0; ch < NCH; ++ch) {
             const int y = y0 + rb;
             const int x = xb + 64 * ch + lane;
-            const float cm = fmaxf(fmaxf(c[rb][ch][0], c[rb][ch][1]), c[rb][ch][2]);
-            const float em = fmaxf(fmaxf(e[rb][ch][0], e[rb][ch][1]), e[rb][ch][2]);
+            const float cm = fmaxf(fmaxf(c[rb][ch], c[rb + 1][ch]), c[rb + 2][ch]);
+            const float em = fmaxf(fmaxf(e[rb][ch], e[rb + 1][ch]), e[rb + 2][ch]);
             const float up = __shfl_up(cm, 1), dn = __shfl_down(cm, 1);
             const float l = lane == 0 ? em : up, r = lane == 63 ? em : dn;
-            const float v = c[rb][ch][1];
+            const float v = c[rb + 1][ch];
             const bool pred = y < H && x < W && pred_of(v, fmaxf(fmaxf(l, cm), r));
             const int slot = lds_wave_append(&L.cnt[1], pred);
             if (pred) cp[slot] = ((uint64_t)(~fkey(v)) << 32) | (uint32_t)(y * W + x);
