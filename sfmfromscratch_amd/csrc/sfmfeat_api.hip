@@ -86,7 +86,9 @@ struct sfm_ctx {
   bool match_direct = false;  // SFMFEAT_MATCH_DIRECT=1: all-pairs exact VALU kernel (A/B checks)
   bool exact_select = false;
   bool serial = false;        // SFMFEAT_SERIAL=1: no aux-stream overlap (diagnostic timings)
-  size_t match_budget = (size_t)2048 << 20;  // SFMFEAT_MATCH_BUDGET_MB: matcher per-pair workspace bound
+  // SFMFEAT_MATCH_BUDGET_MB: matcher per-pair workspace bound (4 GB: 1,575 pairs of 2,500 rows per
+  // sub-launch at 256 admitted targets per row, configs[2]'s 4,096-pair calls in three)
+  size_t match_budget = (size_t)4096 << 20;
   int last_B = 0;             // planes per level of the last extraction
   int last_H = 0, last_W = 0;
   // stage profiling (sfm_profile_*): HIP events bracketing each stage's launches

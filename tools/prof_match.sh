@@ -11,6 +11,6 @@ P2="SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d gpurun_out/pmc_${T}_$i -o run -- python tools/bench_match.py --iters 3 --allpairs > gpurun_out/pmc_${T}_$i.log 2>&1 || exit 1
+  timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d gpurun_out/pmc_${T}_$i -o run -- python tools/bench_match.py --iters 3 ${MATCH_ARGS:---allpairs} > gpurun_out/pmc_${T}_$i.log 2>&1 || exit 1
 done
 echo done
