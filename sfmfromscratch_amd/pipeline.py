@@ -209,12 +209,24 @@ class BatchPipeline:
         torch = self.torch
         ln = self.lanes[self.n % self.inflight]
         self.n += 1
-        ln["stream"].wait_stream(torch.cuda.current_stream(frames.device))
+        cur = torch.cuda.current_stream(frames.device)
+        ln["stream"].wait_stream(cur)
         # the lane reads `frames` after the caller may have dropped it: keep its memory
-        # out of the caching allocator until the lane's work is done
-        frames.record_stream(ln["stream"])
+        # out of the caching allocator until the lane's work is done.  A context-owned lane
+        # stream (lane_streams "context") is destroyed with its context, possibly before the
+        # allocator would query an event recorded by record_stream on it: such lanes hold the
+        # frames instead, released once the caller's stream has waited for the extraction.
+        if self.lane_streams == "context":
+            if ln.get("hold_ev") is not None:
+                cur.wait_event(ln["hold_ev"])
+            ln["hold"] = frames
+        else:
+            frames.record_stream(ln["stream"])
         with torch.cuda.stream(ln["stream"]):
             ln["ex"].extract(frames, out=ln["view"])
+            if self.lane_streams == "context":
+                ln["hold_ev"] = torch.cuda.Event()
+                ln["hold_ev"].record(ln["stream"])
             if hook is not None:
                 hook(ln["slots"], self.B)
             ln["m"].match(ln["slots"], self.pairs, out=ln["mout"])
