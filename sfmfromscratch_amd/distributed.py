@@ -344,7 +344,8 @@ class ChunkedGatherJob:
 
     def __init__(self, extractor_params: dict | None, ratio: float, plan: GatherPlan, rank: int, H: int, W: int,
                  dist=None, inflight: int = 2, exchange: str = "allgather", device: int = 0, group=None,
-                 coalesce: bool | None = None, keep_all_results: bool = False, compact: bool | None = None):
+                 coalesce: bool | None = None, keep_all_results: bool = False, compact: bool | None = None,
+                 lane_streams: str | None = None):
         import torch
         from .pipeline import BatchExtractor, BatchMatcher, SlotTable
         self.torch, self.plan, self.rank, self.dist, self.group = torch, plan, rank, dist, group
@@ -362,14 +363,22 @@ class ChunkedGatherJob:
         dev = torch.device("cuda", device)
         self.dev = dev
         Bx, S, C = plan.chunk, plan.S, plan.C
+        # lane_streams "context": every lane (and the matcher) runs on its context's own HIP
+        # stream, wrapped as a torch ExternalStream (pipeline.BatchPipeline's default layout);
+        # "torch" (default here): streams from torch's pool.  SFM_GATHER_LANE_STREAMS overrides.
+        lane_streams = os.environ.get("SFM_GATHER_LANE_STREAMS", lane_streams or "torch")
+        self.lane_streams = lane_streams
         self.lanes = []
         for _ in range(max(1, inflight)):
             ex = BatchExtractor(extractor_params, device=device)
             ex.reserve(Bx, H, W)
-            self.lanes.append({"ex": ex, "stream": torch.cuda.Stream(device=dev), "pending": None})
+            stream = (torch.cuda.ExternalStream(ex.ctx.stream(), device=dev) if lane_streams == "context"
+                      else torch.cuda.Stream(device=dev))
+            self.lanes.append({"ex": ex, "stream": stream, "pending": None})
         cap = self.cap = self.lanes[0]["ex"].cap
         self.matcher = BatchMatcher(ratio, device=device)  # own context: matches run on their own stream
-        self.mstream = torch.cuda.Stream(device=dev)
+        self.mstream = (torch.cuda.ExternalStream(self.matcher.ctx.stream(), device=dev) if lane_streams == "context"
+                        else torch.cuda.Stream(device=dev))
         if self.halo:
             # local table: slots [0, S) = own frames in order, slot S = rank r+1's first frame
             self.table = SlotTable(torch, S + 1, cap, dev)
