@@ -18,6 +18,40 @@ constexpr int kWave = 64;
 SFM_DEV uint32_t fbits(float f) { return __float_as_uint(f); }
 SFM_DEV float ffrom(uint32_t u) { return __uint_as_float(u); }
 
+// Exact 2x downscale of one value (OpenCV's INTER_AREA-fast rule for exact 2x resizes,
+// pyramid.hip): ((a00 + a01) + (a10 + a11)) * 0.25
+SFM_DEV float down2_px(float a00, float a01, float a10, float a11) {
+  const float t0 = a00 + a01;
+  const float t1 = a10 + a11;
+  return (t0 + t1) * 0.25f;
+}
+// One 8 x 8 block (block row by, column bx) of plane b of a level of size sh x sw -> its
+// 4 x 4, 2 x 2 and 1 x 1 blocks of the next three exact 2x levels (16-B stores into d1)
+SFM_DEV void down2x3_block(const float (&a)[8][8], float* d1, float* d2, float* d3, int b, int sh, int sw,
+                           int by, int bx) {
+  const int w1 = sw >> 1, w2 = sw >> 2, w3 = sw >> 3;
+  const int h1 = sh >> 1, h2 = sh >> 2, h3 = sh >> 3;
+  float l1[4][4], l2[2][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      l1[i][j] = down2_px(a[2 * i][2 * j], a[2 * i][2 * j + 1], a[2 * i + 1][2 * j], a[2 * i + 1][2 * j + 1]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      l2[i][j] = down2_px(l1[2 * i][2 * j], l1[2 * i][2 * j + 1], l1[2 * i + 1][2 * j], l1[2 * i + 1][2 * j + 1]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    *reinterpret_cast<float4*>(d1 + ((int64_t)b * h1 + 4 * by + i) * w1 + 4 * bx) =
+        make_float4(l1[i][0], l1[i][1], l1[i][2], l1[i][3]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    *reinterpret_cast<float2*>(d2 + ((int64_t)b * h2 + 2 * by + i) * w2 + 2 * bx) = make_float2(l2[i][0], l2[i][1]);
+  d3[((int64_t)b * h3 + by) * w3 + bx] = down2_px(l2[0][0], l2[0][1], l2[1][0], l2[1][1]);
+}
+
 // Order-preserving map float -> uint32 (ascending), -0 folded onto +0 (numpy compares
 // them equal; the median/selection only ever needs the value back).
 SFM_DEV uint32_t fkey(float v) {
@@ -241,5 +275,77 @@ SFM_DEV int next_pow2(int v) {
   while (p < v) p <<= 1;
   return p;
 }
+
+// The n (<= blockDim.x) keys of s[0..n) in ascending order, by runs: each wave sorts its 64
+// keys in registers (shuffle bitonic, no LDS), the sorted runs go back to LDS, and every key's
+// final position is its place in its run plus, for each other run, the number of that run's
+// keys below it (a 64-entry binary search; the runs' searches are independent).  The keys are
+// distinct (their low half is the raster index); padding (~0) sorts after every key and is not
+// stored.  Three barriers instead of the bitonic network's ~55 stages (10 block-wide).
+template <int E>  // keys per lane: runs of 64 E keys, n <= E * blockDim.x
+SFM_DEV void run_merge_sort_u64(uint64_t* s, int n) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int RL = 64 * E;  // run length
+  const int nruns = (n + RL - 1) / RL;
+  uint64_t k[E];
+#pragma unroll
+  for (int r = 0; r < E; ++r) {
+    const int i = w * RL + lane * E + r;
+    k[r] = i < n ? s[i] : ~0ull;
+  }
+  if (w < nruns) wave_bitonic_sort_u64<E>(k);
+  __syncthreads();
+  if (w < nruns) {
+#pragma unroll
+    for (int r = 0; r < E; ++r) s[w * RL + lane * E + r] = k[r];
+  }
+  __syncthreads();
+  uint32_t pos[E];
+#pragma unroll
+  for (int r = 0; r < E; ++r) pos[r] = (uint32_t)(lane * E + r);
+  if (w < nruns) {
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      if (v < nruns && v != w) {
+        const uint64_t* run = s + RL * v;
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+          int lo = 0;  // keys of run v below k[r] (RL - 1 at most, then the last entry)
+#pragma unroll
+          for (int step = RL / 2; step >= 1; step >>= 1)
+            if (run[lo + step - 1] < k[r]) lo += step;
+          lo += (lo == RL - 1 && run[lo] < k[r]) ? 1 : 0;
+          pos[r] += (uint32_t)lo;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (w < nruns) {
+#pragma unroll
+    for (int r = 0; r < E; ++r)
+      if (k[r] != ~0ull) s[pos[r]] = k[r];
+  }
+  __syncthreads();
+}
+
+// ascending sort of s[0..n) (distinct keys; padding ~0 sorts last): runs for n <= 2 blockDim.x,
+// else the LDS bitonic network over next_pow2(n) slots (s must hold them)
+SFM_DEV void sort_keys_u64(uint64_t* s, int n) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (n <= nt && nt <= 1024) {
+    run_merge_sort_u64<1>(s, n);
+  } else if (n <= 2 * nt && nt <= 1024) {
+    run_merge_sort_u64<2>(s, n);
+  } else {
+    const int P = next_pow2(n);
+    for (int i = tid; i < P; i += nt)
+      if (i >= n) s[i] = ~0ull;
+    __syncthreads();
+    bitonic_sort_u64(s, P);
+  }
+}
+
+
 
 }  // namespace sfm

@@ -417,6 +417,27 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     const bool grad_in = tx0 - GA >= 0 && tx0 - GA + PWP <= W && ty0 - GA >= 0 && ty0 - GA + PH <= H;
     if (grad_in) sobel(std::false_type{});
     else sobel(std::true_type{});
+    if constexpr (TH == 64) {
+      // fused pyramid: the tile's 8 x 8 blocks of this level -> the next three exact 2x levels
+      // (pyramid.hip k_down2x3's arithmetic, so the levels are bit-identical), one block per
+      // lane of the first wave, read from the image tile in LDS instead of from HBM again
+      float* const d1 = lvs.l[li].down[0];
+      if (d1 != nullptr && tid < 64) {
+        const int bx = tid & 7, by = tid >> 3;
+        const int gy = ty0 + 8 * by, gx = tx0 + 8 * bx;
+        if (gy < H && gx < W) {
+          float a[8][8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float4 lo = *reinterpret_cast<const float4*>(&s_img[GA + 1 + 8 * by + i][XA + 8 * bx]);
+            const float4 hi = *reinterpret_cast<const float4*>(&s_img[GA + 1 + 8 * by + i][XA + 8 * bx + 4]);
+            a[i][0] = lo.x; a[i][1] = lo.y; a[i][2] = lo.z; a[i][3] = lo.w;
+            a[i][4] = hi.x; a[i][5] = hi.y; a[i][6] = hi.z; a[i][7] = hi.w;
+          }
+          down2x3_block(a, d1, lvs.l[li].down[1], lvs.l[li].down[2], b, H, W, gy >> 3, gx >> 3);
+        }
+      }
+    }
     __syncthreads();
     if constexpr (PP) {
       // the image tile is dead: the three products of every gradient (NaiveSIFT.py:61-63, the
@@ -754,6 +775,7 @@ static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipSt
     if (mf == 4) return launch_form<KS, ABL, 5>(g, B, gk, alpha, st);
     bool sm = small > 0;
     for (int k = 0; k < g.n; ++k) {
+      sm = sm && g.l[k].down[0] == nullptr;  // the fused pyramid needs 64-row tiles
       const int64_t t64 = (int64_t)((g.l[k].W + kHT - 1) / kHT) * ((g.l[k].H + kHT - 1) / kHT) * B;
       sm = sm && t64 <= (int64_t)small * 512;
     }

@@ -208,6 +208,9 @@ struct HarrisLevels {
     uint32_t* hist;
     int H, W, tiles_x, ntiles, wg0, nwg;
     SelectScan scan;
+    // fused pyramid (64 x 64 tiles, H and W multiples of 8): the three exact 2x levels below
+    // this one, written from the image tile in LDS (nullptr: none)
+    float* down[3];
   } l[kHarrisMaxLevels];
   int n;
   int prio;  // 1: waves raise their issue priority with the tiles they have left (A/B)

@@ -204,10 +204,7 @@ __global__ void __launch_bounds__(1024) k_match_compact(const RowBest* __restric
   }
   __syncthreads();
   const int m = (int)s_n;
-  const int P = next_pow2(m);
-  for (int i = m + tid; i < P; i += nt) s_k[i] = ~0ull;
-  __syncthreads();
-  bitonic_sort_u64(s_k, P);
+  sort_keys_u64(s_k, m);  // (nndr, row): distinct keys
   for (int i = tid; i < m; i += nt) {
     uint64_t key = s_k[i];
     int r = (int)(uint32_t)key;

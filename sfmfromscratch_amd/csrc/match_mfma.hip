@@ -645,6 +645,106 @@ __global__ void __launch_bounds__(256) k_match_rerank(const float* __restrict__ 
   }
 }
 
+// As k_match_rerank with two (pair, row) items per wavefront, one per half-wave: half h of
+// wave w takes item 2 w + h, four candidates per step (eight lanes each, the same numpy
+// pairwise order), the top-2 merged over the half's four groups.  Half the wavefronts for the
+// same latency chain per item (count, list, ballot, candidate rows).
+__global__ void __launch_bounds__(256) k_match_rerank2(const float* __restrict__ desc,
+                                                       const int32_t* __restrict__ count, int64_t cap,
+                                                       const int32_t* __restrict__ pairs, int P, float ratio,
+                                                       int max_rows, const uint32_t* __restrict__ cand,
+                                                       const int32_t* __restrict__ cand_n,
+                                                       const float* __restrict__ cand_thr,
+                                                       RowBest* __restrict__ rows_out) {
+  __shared__ uint16_t sJ[4][2][kCandCap];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hf = lane >> 5, hl = lane & 31;
+  const int grp = hl >> 3, l8 = lane & 7;
+  const int64_t w = ((int64_t)blockIdx.x * 4 + wv) * 2 + hf;  // (pair, row) of this half-wave
+  const int p = (int)(w / max_rows), row = (int)(w % max_rows);
+  bool ok = p < P;
+  int i1 = 0, i2 = 0, n1 = 0, n2 = 0;
+  if (ok) {
+    i1 = pairs[2 * p];
+    i2 = pairs[2 * p + 1];
+    n1 = count[i1];
+    n2 = count[i2];
+    ok = row < n1 && n2 >= 1;
+  }
+  int c0 = 0, c1 = 0;
+  float thr = 0.0f;
+  if (ok) {
+    const int cw = cand_n[w];
+    c0 = cw & 0xffff;
+    c1 = cw >> 16;
+    ok = c0 <= kHalfCap && c1 <= kHalfCap;  // else k_match_overflow's row
+    thr = cand_thr[w];
+  }
+  const uint32_t* list = cand + w * kCandCap;
+  const float* A = desc + ((int64_t)i1 * cap + row) * 128;
+  const float* Bd = desc + (int64_t)i2 * cap * 128;
+  float a[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) a[i] = ok ? A[8 * i + l8] : 0.0f;
+  int nk = 0;  // window members of this half's item, compacted into sJ[wv][hf] in list order
+  const uint64_t hmask = hf ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int ch = ok ? (h ? c1 : c0) : 0;
+    const int chmax = max(ch, __shfl_xor(ch, 32));  // both halves walk the longer list
+    for (int b0 = 0; b0 < chmax; b0 += 32) {
+      const int idx = b0 + hl;
+      const bool in = idx < ch;
+      const uint32_t e = in ? list[h * kHalfCap + idx] : 0u;
+      const bool keep = in && __uint_as_float(e & 0xffff0000u) <= thr;
+      const uint64_t bal = __ballot(keep) & hmask;
+      const uint64_t below = bal & ((1ull << lane) - 1ull);
+      if (keep) sJ[wv][hf][nk + __popcll(below)] = (uint16_t)(e & 0xffffu);
+      nk += __popcll(bal);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  float e1 = INFINITY, e2 = INFINITY;
+  int j1 = 0x7fffffff;
+  const int nkmax = max(nk, __shfl_xor(nk, 32));
+  for (int s0 = 0; s0 < nkmax; s0 += 4) {
+    const int sidx = s0 + grp;
+    const bool okc = sidx < nk;
+    const int j = okc ? (int)sJ[wv][hf][sidx] : 0;
+    const float* b = Bd + (int64_t)j * 128;
+    float r = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float dd = a[i] - (okc ? b[8 * i + l8] : a[i]);
+      const float sq = dd * dd;
+      r = (i == 0) ? sq : r + sq;
+    }
+    r = r + __shfl_xor(r, 1);  // t01, t23, t45, t67
+    r = r + __shfl_xor(r, 2);  // u0 = t01 + t23, u1 = t45 + t67
+    r = r + __shfl_xor(r, 4);  // u0 + u1
+    if (okc) {
+      if (r < e1 || (r == e1 && j < j1)) { e2 = e1; e1 = r; j1 = j; }
+      else if (r < e2) e2 = r;
+    }
+  }
+#pragma unroll
+  for (int off = 8; off <= 16; off <<= 1) {
+    const float o1 = __shfl_xor(e1, off), o2 = __shfl_xor(e2, off);
+    const int oj = __shfl_xor(j1, off);
+    top2_merge(e1, j1, e2, o1, oj, o2);
+  }
+  if (hl == 0 && ok) {
+    RowBest rb;
+    rb.col = -1;
+    rb.nndr = 0.0f;
+    const float d1 = sqrtf(e1), d2 = sqrtf(e2);
+    if (d2 > 0.0f) {
+      const float nndr = d1 / d2;
+      if (nndr <= ratio) { rb.col = j1; rb.nndr = nndr; }
+    }
+    rows_out[w] = rb;
+  }
+}
+
 // Exact re-rank, eight (pair, row) items per wavefront (A/B variant, kRerank8MaxPairs):
 // for launches of few pairs k_match_rerank's wave per row leaves most lanes idle and pays
 // three dependent memory latencies per row with few waves to hide them:
@@ -858,7 +958,16 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
   else
     SFM_SWEEP(1);
 #undef SFM_SWEEP
-  if (P <= rr8_max)
+  // two (pair, row) items per wavefront above the eight-item kernel's range (round 4: match
+  // stage 0.229 -> 0.223 ms/step at configs[1]); SFMFEAT_RERANK2=0: one item per wavefront (A/B)
+  static const int rr2 = [] {
+    const char* e = getenv("SFMFEAT_RERANK2");
+    return e ? atoi(e) : 1;
+  }();
+  if (rr2 && P > rr8_max)
+    hipLaunchKernelGGL(k_match_rerank2, dim3((unsigned)(((int64_t)P * max_rows + 7) / 8)), dim3(256), 0, st, desc,
+                       count, cap, pairs, P, ratio, max_rows, cand, cand_n, cand_thr, rows);
+  else if (P <= rr8_max)
     hipLaunchKernelGGL(k_match_rerank8, dim3((unsigned)(((int64_t)P * max_rows + 4 * kRrRows - 1) / (4 * kRrRows))),
                        dim3(256), 0, st, desc, count, cap, pairs, P, ratio, max_rows, cand, cand_n, cand_thr, rows);
   else

@@ -64,12 +64,6 @@ __global__ void __launch_bounds__(256) k_down2(const float* __restrict__ src, in
 // every value ((a00 + a01) + (a10 + a11)) * 0.25 of the level above, exactly k_down2's
 // expression, so the levels are bit-identical to three k_down2 launches — without
 // re-reading levels l+1 and l+2.  Needs sh, sw divisible by 8 and 16-B aligned planes.
-SFM_DEV float down2_px(float a00, float a01, float a10, float a11) {
-  const float t0 = a00 + a01;
-  const float t1 = a10 + a11;
-  return (t0 + t1) * 0.25f;
-}
-
 __global__ void __launch_bounds__(256) k_down2x3(const float* __restrict__ src, int sh, int sw,
                                                  float* __restrict__ d1, float* __restrict__ d2,
                                                  float* __restrict__ d3, int B, uint4* __restrict__ z0,
@@ -82,8 +76,6 @@ __global__ void __launch_bounds__(256) k_down2x3(const float* __restrict__ src, 
     for (int64_t i = i0; i < n1; i += gs) z1[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   const int bw = sw >> 3, bh = sh >> 3;
-  const int w1 = sw >> 1, w2 = sw >> 2, w3 = sw >> 3;
-  const int h1 = sh >> 1, h2 = sh >> 2, h3 = sh >> 3;
   const int64_t total = (int64_t)B * bh * bw;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
@@ -100,25 +92,7 @@ __global__ void __launch_bounds__(256) k_down2x3(const float* __restrict__ src, 
       a[i][0] = lo.x; a[i][1] = lo.y; a[i][2] = lo.z; a[i][3] = lo.w;
       a[i][4] = hi.x; a[i][5] = hi.y; a[i][6] = hi.z; a[i][7] = hi.w;
     }
-    float l1[4][4], l2[2][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        l1[i][j] = down2_px(a[2 * i][2 * j], a[2 * i][2 * j + 1], a[2 * i + 1][2 * j], a[2 * i + 1][2 * j + 1]);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        l2[i][j] = down2_px(l1[2 * i][2 * j], l1[2 * i][2 * j + 1], l1[2 * i + 1][2 * j], l1[2 * i + 1][2 * j + 1]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *reinterpret_cast<float4*>(d1 + ((int64_t)b * h1 + 4 * by + i) * w1 + 4 * bx) =
-          make_float4(l1[i][0], l1[i][1], l1[i][2], l1[i][3]);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      *reinterpret_cast<float2*>(d2 + ((int64_t)b * h2 + 2 * by + i) * w2 + 2 * bx) = make_float2(l2[i][0], l2[i][1]);
-    d3[((int64_t)b * h3 + by) * w3 + bx] = down2_px(l2[0][0], l2[0][1], l2[1][0], l2[1][1]);
+    down2x3_block(a, d1, d2, d3, b, sh, sw, by, bx);
   }
 }
 

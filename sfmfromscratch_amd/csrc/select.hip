@@ -25,13 +25,30 @@ namespace sfm {
 constexpr int kTieLdsCap = 4096;
 constexpr int kTopkDirect = 2048;  // candidates sorted whole; above: radix select first
 
+// LDS histogram add (pred lanes add 1 to h[bin]); agg: the lanes on the first active lane's
+// bin fold into one add by that lane (planes where many keys share a bin, e.g. R == 0 runs,
+// otherwise serialise up to 64 same-address atomics per wavefront instruction).
+SFM_DEV void hist_add(uint32_t* h, uint32_t bin, bool pred, bool agg) {
+  if (!agg) {
+    if (pred) atomicAdd(&h[bin], 1u);
+    return;
+  }
+  const uint64_t act = __ballot(pred);
+  if (act == 0) return;
+  const int leader = __ffsll((unsigned long long)act) - 1;
+  const uint32_t b0 = (uint32_t)__shfl((int)bin, leader);
+  const uint64_t same = __ballot(pred && bin == b0);
+  if (pred && bin != b0) atomicAdd(&h[bin], 1u);
+  if (__lane_id() == leader) atomicAdd(&h[b0], (uint32_t)__popcll(same));
+}
+
 // Block radix select over a global array of 64-bit keys on one 32-bit half.
 // use_lo = false: value = key >> 32 over all keys.  use_lo = true: value = key & ~0u over
 // keys whose high half == match_hi.  Finds the value of 0-based rank `rank`; returns it
 // and the residual rank among equal values in *rank_io.
 SFM_DEV uint32_t radix_select_u32(const uint64_t* arr, int64_t m, bool use_lo, uint32_t match_hi,
                                   uint32_t* rank_io, uint32_t* s_h, uint32_t* s_scan,
-                                  uint32_t* s_out) {
+                                  uint32_t* s_out, bool agg = false) {
   const int tid = threadIdx.x, nt = blockDim.x;
   uint32_t prefix = 0, mask = 0, rank = *rank_io;
   const int shifts[3] = {20, 8, 0};
@@ -40,16 +57,11 @@ SFM_DEV uint32_t radix_select_u32(const uint64_t* arr, int64_t m, bool use_lo, u
     for (int i = tid; i < kHistBins; i += nt) s_h[i] = 0u;
     __syncthreads();
     for (int64_t i = tid; i < m; i += nt) {
-      uint64_t key = arr[i];
-      uint32_t hi = (uint32_t)(key >> 32);
-      uint32_t v;
-      if (use_lo) {
-        if (hi != match_hi) continue;
-        v = (uint32_t)key;
-      } else {
-        v = hi;
-      }
-      if ((v & mask) == prefix) atomicAdd(&s_h[(v >> shifts[d]) & dmasks[d]], 1u);
+      const uint64_t key = arr[i];
+      const uint32_t hi = (uint32_t)(key >> 32);
+      const uint32_t v = use_lo ? (uint32_t)key : hi;
+      const bool in = (!use_lo || hi == match_hi) && (v & mask) == prefix;
+      hist_add(s_h, (v >> shifts[d]) & dmasks[d], in, agg);
     }
     __syncthreads();
     find_bin(s_h, kHistBins, rank, s_scan, s_out);
@@ -67,7 +79,7 @@ SFM_DEV uint32_t radix_select_u32(const uint64_t* arr, int64_t m, bool use_lo, u
 // real key's).  No global re-reads between the digit passes.
 template <int R>
 SFM_DEV uint32_t radix_select_regs(const uint64_t (&kr)[R], int64_t m, uint32_t* rank_io, uint32_t* s_h,
-                                   uint32_t* s_scan, uint32_t* s_out) {
+                                   uint32_t* s_scan, uint32_t* s_out, bool agg = false) {
   const int tid = threadIdx.x, nt = blockDim.x;
   uint32_t prefix = 0, mask = 0, rank = *rank_io;
   const int shifts[3] = {20, 8, 0};
@@ -78,7 +90,7 @@ SFM_DEV uint32_t radix_select_regs(const uint64_t (&kr)[R], int64_t m, uint32_t*
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const uint32_t v = (uint32_t)(kr[j] >> 32);
-      if ((int64_t)tid + (int64_t)nt * j < m && (v & mask) == prefix) atomicAdd(&s_h[(v >> shifts[d]) & dmasks[d]], 1u);
+      hist_add(s_h, (v >> shifts[d]) & dmasks[d], (int64_t)tid + (int64_t)nt * j < m && (v & mask) == prefix, agg);
     }
     __syncthreads();
     find_bin(s_h, kHistBins, rank, s_scan, s_out);
@@ -102,80 +114,11 @@ struct SelectLds {
   uint32_t* cnt;   // 2
 };
 
-// The n (<= blockDim.x) keys of s[0..n) in ascending order, by runs: each wave sorts its 64
-// keys in registers (shuffle bitonic, no LDS), the sorted runs go back to LDS, and every key's
-// final position is its place in its run plus, for each other run, the number of that run's
-// keys below it (a 64-entry binary search; the runs' searches are independent).  The keys are
-// distinct (their low half is the raster index); padding (~0) sorts after every key and is not
-// stored.  Three barriers instead of the bitonic network's ~55 stages (10 block-wide).
-template <int E>  // keys per lane: runs of 64 E keys, n <= E * blockDim.x
-SFM_DEV void run_merge_sort_u64(uint64_t* s, int n) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  constexpr int RL = 64 * E;  // run length
-  const int nruns = (n + RL - 1) / RL;
-  uint64_t k[E];
-#pragma unroll
-  for (int r = 0; r < E; ++r) {
-    const int i = w * RL + lane * E + r;
-    k[r] = i < n ? s[i] : ~0ull;
-  }
-  if (w < nruns) wave_bitonic_sort_u64<E>(k);
-  __syncthreads();
-  if (w < nruns) {
-#pragma unroll
-    for (int r = 0; r < E; ++r) s[w * RL + lane * E + r] = k[r];
-  }
-  __syncthreads();
-  uint32_t pos[E];
-#pragma unroll
-  for (int r = 0; r < E; ++r) pos[r] = (uint32_t)(lane * E + r);
-  if (w < nruns) {
-#pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      if (v < nruns && v != w) {
-        const uint64_t* run = s + RL * v;
-#pragma unroll
-        for (int r = 0; r < E; ++r) {
-          int lo = 0;  // keys of run v below k[r] (RL - 1 at most, then the last entry)
-#pragma unroll
-          for (int step = RL / 2; step >= 1; step >>= 1)
-            if (run[lo + step - 1] < k[r]) lo += step;
-          lo += (lo == RL - 1 && run[lo] < k[r]) ? 1 : 0;
-          pos[r] += (uint32_t)lo;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  if (w < nruns) {
-#pragma unroll
-    for (int r = 0; r < E; ++r)
-      if (k[r] != ~0ull) s[pos[r]] = k[r];
-  }
-  __syncthreads();
-}
-
-// ascending sort of s[0..n) (distinct keys; padding ~0 sorts last): runs for n <= 2 blockDim.x,
-// else the LDS bitonic network over next_pow2(n) slots (s must hold them)
-SFM_DEV void sort_keys_u64(uint64_t* s, int n) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-  if (n <= nt && nt <= 1024) {
-    run_merge_sort_u64<1>(s, n);
-  } else if (n <= 2 * nt && nt <= 1024) {
-    run_merge_sort_u64<2>(s, n);
-  } else {
-    const int P = next_pow2(n);
-    for (int i = tid; i < P; i += nt)
-      if (i >= n) s[i] = ~0ull;
-    __syncthreads();
-    bitonic_sort_u64(s, P);
-  }
-}
-
 // The kk (>= 1) smallest of the C keys cp[0..C) into L.sel[0..kk), ascending (tp: per-plane
 // scratch for tie lists that overflow LDS).
 // abl (timing ablations, results wrong by design; SFMFEAT_SELECT_ABL): 1 no final sort, 2 no
-// radix select (every key counts as below the k-th)
+// radix select (every key counts as below the k-th); k_select: 4 no exact median, 8 no exact NMS;
+// 16 (a correct variant, A/B): wave-aggregated histogram adds (hist_add)
 SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, const SelectLds& L, int abl = 0) {
   const int tid = threadIdx.x, nt = blockDim.x;
   if (C <= kTopkDirect) {
@@ -204,7 +147,7 @@ SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, co
       const int64_t i = tid + (int64_t)nt * j;
       kr[j] = i < C ? cp[i] : ~0ull;
     }
-    T = (abl & 2) ? 0xffffffffu : radix_select_regs(kr, C, &rank, L.h, L.scan, L.out);
+    T = (abl & 2) ? 0xffffffffu : radix_select_regs(kr, C, &rank, L.h, L.scan, L.out, (abl & 16) != 0);
     if (tid == 0) {
       L.cnt[0] = 0u;
       L.cnt[1] = 0u;
@@ -214,7 +157,7 @@ SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, co
     for (int j = 0; j < kRegKeys; ++j)
       if (tid + (int64_t)nt * j < C) part(kr[j]);
   } else {
-    T = radix_select_u32(cp, C, false, 0u, &rank, L.h, L.scan, L.out);
+    T = radix_select_u32(cp, C, false, 0u, &rank, L.h, L.scan, L.out, (abl & 16) != 0);
     if (tid == 0) {
       L.cnt[0] = 0u;
       L.cnt[1] = 0u;
@@ -231,7 +174,7 @@ SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, co
     for (uint32_t i = tid; i < need; i += nt) L.sel[nless + i] = L.tie[i];
   } else {
     uint32_t r2 = rank;
-    const uint32_t Tlo = radix_select_u32(tp, ntie, true, T, &r2, L.h, L.scan, L.out);
+    const uint32_t Tlo = radix_select_u32(tp, ntie, true, T, &r2, L.h, L.scan, L.out, (abl & 16) != 0);
     for (int64_t i = tid; i < ntie; i += nt) {
       const uint64_t key = tp[i];
       if ((uint32_t)key <= Tlo) L.sel[atomicAdd(&L.cnt[0], 1u)] = key;
@@ -287,14 +230,15 @@ SFM_DEV int lds_wave_append(uint32_t* counter, bool pred) {
 // and of rank r2 in bucket b2 histogrammed in the two halves of s_h in one list pass, then
 // digit 3 (10 bits) likewise (as select_in_list twice, in half the passes).
 SFM_DEV void select_pair_in_list(const uint32_t* lp, int64_t m, uint32_t b1, uint32_t r1, uint32_t b2, uint32_t r2,
-                                 const SelectLds& L, uint32_t* key1, uint32_t* key2) {
+                                 const SelectLds& L, uint32_t* key1, uint32_t* key2, bool agg) {
   const int tid = threadIdx.x, nt = blockDim.x;
   for (int i = tid; i < kHistBins; i += nt) L.h[i] = 0u;
   __syncthreads();
   for (int64_t i = tid; i < m; i += nt) {
     const uint32_t k = lp[i];
-    if ((k >> 21) == b1) atomicAdd(&L.h[(k >> 10) & 0x7ffu], 1u);
-    if ((k >> 21) == b2) atomicAdd(&L.h[2048 + ((k >> 10) & 0x7ffu)], 1u);
+    const bool in2 = (k >> 21) == b2;  // b1 == b2 is possible: both halves count the key
+    hist_add(L.h, (k >> 10) & 0x7ffu, (k >> 21) == b1, agg);
+    hist_add(L.h, 2048 + ((k >> 10) & 0x7ffu), in2, agg);
   }
   __syncthreads();
   find_bin(L.h, 2048, r1, L.scan, L.out);
@@ -309,8 +253,8 @@ SFM_DEV void select_pair_in_list(const uint32_t* lp, int64_t m, uint32_t b1, uin
   __syncthreads();
   for (int64_t i = tid; i < m; i += nt) {
     const uint32_t k = lp[i];
-    if ((k >> 10) == pre1) atomicAdd(&L.h[k & 0x3ffu], 1u);
-    if ((k >> 10) == pre2) atomicAdd(&L.h[1024 + (k & 0x3ffu)], 1u);
+    hist_add(L.h, k & 0x3ffu, (k >> 10) == pre1, agg);
+    hist_add(L.h, 1024 + (k & 0x3ffu), (k >> 10) == pre2, agg);
   }
   __syncthreads();
   find_bin(L.h, 1024, r1, L.scan, L.out);
@@ -324,7 +268,8 @@ SFM_DEV void select_pair_in_list(const uint32_t* lp, int64_t m, uint32_t b1, uin
 // np.median of the plane (NaiveSIFT.py:91): the keys of the two digit-1 buckets holding the
 // middle ranks (from the Harris histogram's select scan) are collected into `list`, then
 // digits 2 and 3 resolved by select_in_list.  Even n: float32 (v[n/2-1] + v[n/2]) / 2.
-SFM_DEV float exact_median(const float* Rp, int64_t n, const MedianState& s, uint32_t* list, const SelectLds& L) {
+SFM_DEV float exact_median(const float* Rp, int64_t n, const MedianState& s, uint32_t* list, const SelectLds& L,
+                           bool agg) {
   const int tid = threadIdx.x, nt = blockDim.x;
   if (tid == 0) L.cnt[0] = 0u;
   __syncthreads();
@@ -352,7 +297,7 @@ SFM_DEV float exact_median(const float* Rp, int64_t n, const MedianState& s, uin
   __syncthreads();
   if (s.odd) return fkey_inv(select_in_list(list, m, b1, s.rank[0], L.h, L.scan, L.out));
   uint32_t key1, key2;
-  select_pair_in_list(list, m, b1, s.rank[0], b2, s.rank[1], L, &key1, &key2);
+  select_pair_in_list(list, m, b1, s.rank[0], b2, s.rank[1], L, &key1, &key2, agg);
   const float v1 = fkey_inv(key1);
   const float v2 = fkey_inv(key2);
   const float sum = v1 + v2;
@@ -484,9 +429,11 @@ __global__ void __launch_bounds__(1024) k_select(SelectLevels g, int kcap, int k
     // cannot certify (fewer than k candidates, or the k-th not above the median's bucket)
     if (tid == 0) state[b].fallback = 1u;
   }
-  const float med = exact_median(R + (int64_t)b * n, n, s, medlist + (int64_t)b * n, L);
+  // abl 4: no exact median (the median's bucket start instead), 8: no exact NMS (no candidates)
+  const float med = (abl & 4) ? fkey_inv(s.bucket[0] << (32 - kMedBits1))
+                              : exact_median(R + (int64_t)b * n, n, s, medlist + (int64_t)b * n, L, (abl & 16) != 0);
   if (tid == 0) state[b].median = med;
-  const int64_t C = exact_nms(R + (int64_t)b * n, H, W, kh, med, cp, L);
+  const int64_t C = (abl & 8) ? 0 : exact_nms(R + (int64_t)b * n, H, W, kh, med, cp, L);
   const int kk = (int)((int64_t)k < C ? (int64_t)k : C);
   if (kk <= 0) {
     if (tid == 0) kp.count[b] = 0;

@@ -299,15 +299,21 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     return e && atoi(e) != 0;
   }();
   bool zeroed = fill_launches;
-  {
-    StageScope sc(c, SFM_PROF_PYRAMID, st);
-    int64_t off = 0;
-    for (int l = 1; l < L; ++l) {
-      float* dst = as<float>(c->d_lvl) + off;
-      lvl[l] = dst;
-      off += (int64_t)B * lv[l].h * lv[l].w;
-    }
-    for (int l = 1; l < L;) {
+  // Levels 1-3 exact 2x below level 0 (H, W multiples of 8): the level-0 Harris launch writes
+  // them from its image tiles in LDS (level 0 is read from HBM once; round 4: 35.6k -> 37.3k
+  // img/s at configs[1]), levels >= 4 follow that launch, and the histograms / counters take
+  // the fill launches instead of k_down2x3's side job.  SFMFEAT_PYR_FUSED=0: k_down2x3 (A/B).
+  static const bool pyr_fused_env = [] {
+    const char* e = getenv("SFMFEAT_PYR_FUSED");
+    return !e || atoi(e) != 0;
+  }();
+  const bool pyr_fused = pyr_fused_env && L >= 4 && H % 8 == 0 && W % 8 == 0 && lv[1].h * 2 == H &&
+                         lv[1].w * 2 == W && lv[2].h * 4 == H && lv[2].w * 4 == W && lv[3].h * 8 == H &&
+                         lv[3].w * 8 == W;
+  // levels [from, L) from their predecessors: three exact 2x levels from one read of their
+  // source where the sizes allow, else one resize per level
+  auto pyramid_from = [&](int from) {
+    for (int l = from; l < L;) {
       // three exact 2x levels from one read of their source where the sizes allow
       const auto& s = lv[l - 1];
       const bool x2 = l + 2 < L && lv[l].h * 2 == s.h && lv[l].w * 2 == s.w && lv[l + 1].h * 4 == s.h &&
@@ -322,6 +328,16 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
       launch_resize(lvl[l - 1], s.h, s.w, const_cast<float*>(lvl[l]), lv[l].h, lv[l].w, B, st);
       ++l;
     }
+  };
+  {
+    StageScope sc(c, SFM_PROF_PYRAMID, st);
+    int64_t off = 0;
+    for (int l = 1; l < L; ++l) {
+      float* dst = as<float>(c->d_lvl) + off;
+      lvl[l] = dst;
+      off += (int64_t)B * lv[l].h * lv[l].w;
+    }
+    if (!pyr_fused) pyramid_from(1);
   }
   if (!zeroed || fill_launches) {
     HIPCHK(c, hipMemsetAsync(c->d_hist.p, 0, hist_bytes, st));
@@ -435,8 +451,18 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
         q.H = lv[l].h;
         q.W = lv[l].w;
         q.scan = SelectScan{e.med, medcnt + e.co, donecnt + e.co, vmin, e.exact ? 1 : 0};
+        q.down[0] = q.down[1] = q.down[2] = nullptr;
+        if (pyr_fused && l == 0) {
+          q.down[0] = const_cast<float*>(lvl[1]);
+          q.down[1] = const_cast<float*>(lvl[2]);
+          q.down[2] = const_cast<float*>(lvl[3]);
+        }
       }
       if (!(l0 > 0 && (skip & 16))) launch_harris_levels(g, B, as<float>(c->d_gauss), c->p.gaussian_size, alpha, st);
+    }
+    if (pyr_fused && l0 == 0 && L > 4) {
+      StageScope sc(c, SFM_PROF_PYRAMID, st);
+      pyramid_from(4);
     }
     if (gate_level >= l0 && gate_level < l1 && (rc = release_gate())) return rc;
     for (int l = l0; l < l1; ++l) {
