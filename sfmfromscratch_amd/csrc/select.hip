@@ -56,12 +56,22 @@ SFM_DEV uint32_t radix_select_u32(const uint64_t* arr, int64_t m, bool use_lo, u
   for (int d = 0; d < 3; ++d) {
     for (int i = tid; i < kHistBins; i += nt) s_h[i] = 0u;
     __syncthreads();
-    for (int64_t i = tid; i < m; i += nt) {
-      const uint64_t key = arr[i];
-      const uint32_t hi = (uint32_t)(key >> 32);
-      const uint32_t v = use_lo ? (uint32_t)key : hi;
-      const bool in = (!use_lo || hi == match_hi) && (v & mask) == prefix;
-      hist_add(s_h, (v >> shifts[d]) & dmasks[d], in, agg);
+    constexpr int U = 8;  // loads in flight per thread
+    for (int64_t base = 0; base < m; base += (int64_t)nt * U) {
+      uint64_t kb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = base + tid + (int64_t)nt * u;
+        kb[u] = i < m ? arr[i] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint64_t key = kb[u];
+        const uint32_t hi = (uint32_t)(key >> 32);
+        const uint32_t v = use_lo ? (uint32_t)key : hi;
+        const bool in = base + tid + (int64_t)nt * u < m && (!use_lo || hi == match_hi) && (v & mask) == prefix;
+        hist_add(s_h, (v >> shifts[d]) & dmasks[d], in, agg);
+      }
     }
     __syncthreads();
     find_bin(s_h, kHistBins, rank, s_scan, s_out);
@@ -163,7 +173,18 @@ SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, co
       L.cnt[1] = 0u;
     }
     __syncthreads();
-    for (int64_t i = tid; i < C; i += nt) part(cp[i]);
+    constexpr int U = 8;  // loads in flight per thread
+    for (int64_t base = 0; base < C; base += (int64_t)nt * U) {
+      uint64_t kb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = base + tid + (int64_t)nt * u;
+        kb[u] = i < C ? cp[i] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (base + tid + (int64_t)nt * u < C) part(kb[u]);
+    }
   }
   __syncthreads();
   const uint32_t nless = (abl & 2) ? min(L.cnt[0], (uint32_t)kk) : L.cnt[0];
@@ -229,13 +250,17 @@ SFM_DEV int lds_wave_append(uint32_t* counter, bool pred) {
 // Both middle keys from the collected list at once: digit 2 (11 bits) of rank r1 in bucket b1
 // and of rank r2 in bucket b2 histogrammed in the two halves of s_h in one list pass, then
 // digit 3 (10 bits) likewise (as select_in_list twice, in half the passes).
-SFM_DEV void select_pair_in_list(const uint32_t* lp, int64_t m, uint32_t b1, uint32_t r1, uint32_t b2, uint32_t r2,
-                                 const SelectLds& L, uint32_t* key1, uint32_t* key2, bool agg) {
+// The list's first kMedLdsCap keys live in LDS (ll), the rest in global memory (lp, same index).
+constexpr int kMedLdsCap = (kTopkLdsCap + kTieLdsCap) * 2;  // u32 keys over the sel + tie areas
+
+SFM_DEV void select_pair_in_list(const uint32_t* ll, const uint32_t* lp, int64_t m, uint32_t b1, uint32_t r1,
+                                 uint32_t b2, uint32_t r2, const SelectLds& L, uint32_t* key1, uint32_t* key2,
+                                 bool agg) {
   const int tid = threadIdx.x, nt = blockDim.x;
   for (int i = tid; i < kHistBins; i += nt) L.h[i] = 0u;
   __syncthreads();
   for (int64_t i = tid; i < m; i += nt) {
-    const uint32_t k = lp[i];
+    const uint32_t k = i < kMedLdsCap ? ll[i] : lp[i];
     const bool in2 = (k >> 21) == b2;  // b1 == b2 is possible: both halves count the key
     hist_add(L.h, (k >> 10) & 0x7ffu, (k >> 21) == b1, agg);
     hist_add(L.h, 2048 + ((k >> 10) & 0x7ffu), in2, agg);
@@ -252,7 +277,7 @@ SFM_DEV void select_pair_in_list(const uint32_t* lp, int64_t m, uint32_t b1, uin
   for (int i = tid; i < 2048; i += nt) L.h[i] = 0u;
   __syncthreads();
   for (int64_t i = tid; i < m; i += nt) {
-    const uint32_t k = lp[i];
+    const uint32_t k = i < kMedLdsCap ? ll[i] : lp[i];
     hist_add(L.h, k & 0x3ffu, (k >> 10) == pre1, agg);
     hist_add(L.h, 1024 + (k & 0x3ffu), (k >> 10) == pre2, agg);
   }
@@ -266,38 +291,67 @@ SFM_DEV void select_pair_in_list(const uint32_t* lp, int64_t m, uint32_t b1, uin
 }
 
 // np.median of the plane (NaiveSIFT.py:91): the keys of the two digit-1 buckets holding the
-// middle ranks (from the Harris histogram's select scan) are collected into `list`, then
-// digits 2 and 3 resolved by select_in_list.  Even n: float32 (v[n/2-1] + v[n/2]) / 2.
+// middle ranks (from the Harris histogram's select scan) are collected into a list whose
+// first kMedLdsCap keys stay in LDS (the top-k areas are free until the exact NMS), the rest
+// in `list`; then digits 2 and 3 are resolved from it.  Even n: float32 (v[n/2-1] + v[n/2]) / 2.
+// The plane is read with 16-B loads (8 per thread in flight) when it is 16-B aligned.
 SFM_DEV float exact_median(const float* Rp, int64_t n, const MedianState& s, uint32_t* list, const SelectLds& L,
                            bool agg) {
   const int tid = threadIdx.x, nt = blockDim.x;
+  uint32_t* const ll = reinterpret_cast<uint32_t*>(L.sel);
   if (tid == 0) L.cnt[0] = 0u;
   __syncthreads();
   const uint32_t b1 = s.bucket[0], b2 = s.bucket[1];
-  constexpr int U = 8;  // loads in flight per thread
-  for (int64_t base = 0; base < n; base += (int64_t)nt * U) {
-    float v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = base + tid + (int64_t)nt * u;
-      v[u] = i < n ? Rp[i] : 0.0f;
+  auto put = [&](uint32_t key, bool valid) {
+    const uint32_t d = key >> (32 - kMedBits1);
+    const bool in = valid && (d == b1 || d == b2);
+    const int slot = lds_wave_append(&L.cnt[0], in);
+    if (in) {
+      if (slot < kMedLdsCap) ll[slot] = key;
+      else list[slot] = key;
     }
+  };
+  constexpr int U = 8;  // loads in flight per thread
+  if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(Rp) & 15) == 0) {
+    const float4* R4 = reinterpret_cast<const float4*>(Rp);
+    const int64_t n4 = n >> 2;
+    for (int64_t base = 0; base < n4; base += (int64_t)nt * U) {
+      float4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = base + tid + (int64_t)nt * u;
-      const uint32_t key = fkey(v[u]);
-      const uint32_t d = key >> (32 - kMedBits1);
-      const bool in = i < n && (d == b1 || d == b2);
-      const int slot = lds_wave_append(&L.cnt[0], in);
-      if (in) list[slot] = key;
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = base + tid + (int64_t)nt * u;
+        v[u] = i < n4 ? R4[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = base + tid + (int64_t)nt * u < n4;
+        put(fkey(v[u].x), ok);
+        put(fkey(v[u].y), ok);
+        put(fkey(v[u].z), ok);
+        put(fkey(v[u].w), ok);
+      }
+    }
+  } else {
+    for (int64_t base = 0; base < n; base += (int64_t)nt * U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = base + tid + (int64_t)nt * u;
+        v[u] = i < n ? Rp[i] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) put(fkey(v[u]), base + tid + (int64_t)nt * u < n);
     }
   }
   __syncthreads();
   const int64_t m = (int64_t)L.cnt[0];
   __syncthreads();
-  if (s.odd) return fkey_inv(select_in_list(list, m, b1, s.rank[0], L.h, L.scan, L.out));
   uint32_t key1, key2;
-  select_pair_in_list(list, m, b1, s.rank[0], b2, s.rank[1], L, &key1, &key2, agg);
+  if (s.odd) {  // one middle rank: the pair search on (b1, rank) twice
+    select_pair_in_list(ll, list, m, b1, s.rank[0], b1, s.rank[0], L, &key1, &key2, agg);
+    return fkey_inv(key1);
+  }
+  select_pair_in_list(ll, list, m, b1, s.rank[0], b2, s.rank[1], L, &key1, &key2, agg);
   const float v1 = fkey_inv(key1);
   const float v2 = fkey_inv(key2);
   const float sum = v1 + v2;
@@ -316,7 +370,54 @@ SFM_DEV int64_t exact_nms(const float* Rp, int H, int W, int kh, float med, uint
   if (tid == 0) L.cnt[1] = 0u;
   __syncthreads();
   auto pred_of = [&](float v, float m) { return (v < med) ? (v == 0.0f) : (v == m); };
-  if (kh == 1) {
+  if (kh == 1 && (W & 3) == 0 && (reinterpret_cast<uintptr_t>(Rp) & 15) == 0) {
+    // as below with 16-B loads: lane l of chunk ch owns columns x0 .. x0 + 3 (x0 = xb + 256 ch
+    // + 4 l); the window's outer columns come from the neighbouring lanes' column maxima
+    // (the chunk's edge lanes load the column beyond it)
+    constexpr int NCH = 1, RB = 4;
+    for (int y0 = wid * RB; y0 < H; y0 += nw * RB) {
+      for (int xb = 0; xb < W; xb += 256 * NCH) {
+        float4 c[RB + 2][NCH];
+        float e[RB + 2][NCH];
+#pragma unroll
+        for (int rr = 0; rr < RB + 2; ++rr) {
+          const int yy = y0 - 1 + rr;
+          const bool rok = yy >= 0 && yy < H;
+#pragma unroll
+          for (int ch = 0; ch < NCH; ++ch) {
+            const int x0 = xb + 256 * ch + 4 * lane;
+            const int xe = lane == 0 ? x0 - 1 : x0 + 4;  // edge lanes: the column beyond the chunk
+            c[rr][ch] = (rok && x0 < W) ? *reinterpret_cast<const float4*>(Rp + (int64_t)yy * W + x0)
+                                        : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+            e[rr][ch] = (rok && (lane == 0 || lane == 63) && xe >= 0 && xe < W) ? Rp[(int64_t)yy * W + xe] : -INFINITY;
+          }
+        }
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+          for (int ch = 0; ch < NCH; ++ch) {
+            const int y = y0 + rb;
+            const int x0 = xb + 256 * ch + 4 * lane;
+            const float4 a = c[rb][ch], m = c[rb + 1][ch], z = c[rb + 2][ch];
+            const float c0 = fmaxf(fmaxf(a.x, m.x), z.x), c1 = fmaxf(fmaxf(a.y, m.y), z.y);
+            const float c2 = fmaxf(fmaxf(a.z, m.z), z.z), c3 = fmaxf(fmaxf(a.w, m.w), z.w);
+            const float em = fmaxf(fmaxf(e[rb][ch], e[rb + 1][ch]), e[rb + 2][ch]);
+            const float up = __shfl_up(c3, 1), dn = __shfl_down(c0, 1);
+            const float l = lane == 0 ? em : up, r = lane == 63 ? em : dn;
+            const float w0 = fmaxf(fmaxf(l, c0), c1), w1 = fmaxf(fmaxf(c0, c1), c2);
+            const float w2 = fmaxf(fmaxf(c1, c2), c3), w3 = fmaxf(fmaxf(c2, c3), r);
+            const bool rowok = y < H && x0 < W;
+            const float vv[4] = {m.x, m.y, m.z, m.w}, ww[4] = {w0, w1, w2, w3};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const bool pred = rowok && pred_of(vv[j], ww[j]);
+              const int slot = lds_wave_append(&L.cnt[1], pred);
+              if (pred) cp[slot] = ((uint64_t)(~fkey(vv[j])) << 32) | (uint32_t)(y * W + x0 + j);
+            }
+          }
+      }
+    }
+  } else if (kh == 1) {
     // RB output rows per wavefront iteration from RB + 2 image rows loaded once (every load
     // of the iteration in flight together)
     constexpr int NCH = 2, RB = 4;

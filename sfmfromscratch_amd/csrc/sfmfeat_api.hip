@@ -374,6 +374,14 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     size_t co;
     bool exact;
   };
+  // levels of fewer than 128 x kcap pixels (the certified select's vmin) skip certification:
+  // they hardly ever certify (4K level 3 never did), and the attempt costs a certified NMS
+  // pass and a top-k before the exact path (configs[4] 8.85k -> 9.02k img/s with 128 against
+  // 64; 1080p takes the same levels either way).  SFMFEAT_EXACT_PX=n: n x kcap (A/B)
+  static const int exact_px = [] {
+    const char* e = getenv("SFMFEAT_EXACT_PX");
+    return e ? atoi(e) : 128;
+  }();
   std::vector<LevelBufs> lb(L);
   int64_t plane_off = 0;  // element offset of level l's planes in the per-level R / candidates
   for (int l = 0; l < L; ++l) {
@@ -389,9 +397,9 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     e.kp.y = as<int32_t>(c->d_kpy) + ko;
     e.kp.conf = as<float>(c->d_kpc) + ko;
     e.kp.count = as<int32_t>(c->d_lc) + (size_t)l * B;
-    // levels too small to hold ~k window maxima above the median go straight to the exact
-    // path (a size-only decision: no host synchronisation)
-    e.exact = c->exact_select || (int64_t)h * w < (int64_t)64 * c->kcap;
+    // levels too small to certify go straight to the exact path (a size-only decision: no
+    // host synchronisation)
+    e.exact = c->exact_select || (int64_t)h * w < (int64_t)exact_px * c->kcap;
   }
   auto select_level = [&](int l, hipStream_t s) {  // top-k, exact path in the same launch
     const LevelBufs& e = lb[l];
