@@ -288,18 +288,26 @@ def main():
         px = sum(h * w for h, w in levels) * B * nsteps
         pair_elems = sum(int(counts[i]) * int(counts[j]) for i, j in pairs_np) * 128 * nsteps
         # k_down2x3 reads level 0 once and writes levels 1..3 (one launch); a 5th level is
-        # one k_down2 from level 3
+        # one k_down2 from level 3.  Levels 1..3 exact 2x (H, W multiples of 8): the level-0
+        # k_harris launch writes them from its image tiles (sfmfeat_api.hip, SFMFEAT_PYR_FUSED),
+        # so their bytes move to the Harris stage and the pyramid stage keeps levels >= 4
         A = [h * w for h, w in levels]
-        pyr_px = A[0] + sum(A[1:4]) + sum(A[l - 1] + A[l] for l in range(4, len(A)))
+        fused = (len(A) >= 4 and H % 8 == 0 and W % 8 == 0 and
+                 os.environ.get("SFMFEAT_PYR_FUSED", "1") != "0")
+        tail_px = sum(A[l - 1] + A[l] for l in range(4, len(A)))
+        pyr_px = tail_px if fused else A[0] + sum(A[1:4]) + tail_px
         pyr_bytes = 4.0 * pyr_px * B * nsteps
-        return {
+        harris_bytes = 8.0 * px + (4.0 * sum(A[1:4]) * B * nsteps if fused else 0.0)
+        work = {
             # VALU-bound: 328 flop/px of separate mul/add-class ops; bytes: read
-            # the level, write R
-            "harris": ("valu", HARRIS_FLOP_PER_PX * px / 1e12, "TFLOP/s", PEAK_F32_TFLOPS, 8.0 * px),
+            # the level, write R (+ the fused pyramid levels)
+            "harris": ("valu", HARRIS_FLOP_PER_PX * px / 1e12, "TFLOP/s", PEAK_F32_TFLOPS, harris_bytes),
             "match": ("mfma", MATCH_FLOP_PER_ELEM * pair_elems / 1e12, "TFLOP/s", PEAK_MATCH_TFLOPS, None),
             "nms": ("hbm", 4.0 * px / 1e9, "GB/s", PEAK_HBM_GBS, 4.0 * px),          # one read of R
-            "pyramid": ("hbm", pyr_bytes / 1e9, "GB/s", PEAK_HBM_GBS, pyr_bytes),
         }
+        if pyr_px > 0:
+            work["pyramid"] = ("hbm", pyr_bytes / 1e9, "GB/s", PEAK_HBM_GBS, pyr_bytes)
+        return work
 
     def level_keypoints():
         """Keypoints per pyramid level over the batch (host-path extraction of the same frames,
@@ -360,6 +368,14 @@ def main():
                 ach = amount / (ms / 1e3)
                 st.update({"bound": bound, "achieved": round(ach, 3), "unit": unit, "frac": round(ach / peak, 4)})
             stages[k] = st
+        if "pyramid" in stages and "pyramid" not in work:
+            stages["pyramid"]["note"] = ("levels 1-3 written by the level-0 k_harris launch (their bytes are "
+                                         "in the harris stage); the stage's events bracket no launch here")
+        if "topk" in stages:
+            stages["topk"].update({"bound": "latency", "workgroups_per_launch": B,
+                                   "note": "one 1,024-thread workgroup per plane and level: a dependent chain of "
+                                           "barriers (radix digit passes, run sorts; the exact path's plane "
+                                           "reads on exact levels); no byte or flop roofline applies"})
         dom = max((k for k in prof_all if k in work and prof_all[k][1]), key=lambda k: prof_all[k][0])
         prof_enable(False)
         prof_read()
