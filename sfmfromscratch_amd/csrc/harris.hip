@@ -770,12 +770,15 @@ static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipSt
   // / every level
   static const int mf = env_int("SFMFEAT_HARRIS_MF", kHarrisMfma);
   if constexpr (KS == 7) {  // the alternative forms are built for the 7 x 7 window only
+    // the fused pyramid (levels with down[0] set) is validated in form 0 only
+    bool fused = false;
+    for (int k = 0; k < g.n; ++k) fused = fused || g.l[k].down[0] != nullptr;
+    if (fused) return launch_form<KS, ABL, 0>(g, B, gk, alpha, st);
     if (npair == 1) return launch_form<KS, ABL, 1>(g, B, gk, alpha, st);
     if (mf == 2) return launch_form<KS, ABL, 4>(g, B, gk, alpha, st);
     if (mf == 4) return launch_form<KS, ABL, 5>(g, B, gk, alpha, st);
     bool sm = small > 0;
     for (int k = 0; k < g.n; ++k) {
-      sm = sm && g.l[k].down[0] == nullptr;  // the fused pyramid needs 64-row tiles
       const int64_t t64 = (int64_t)((g.l[k].W + kHT - 1) / kHT) * ((g.l[k].H + kHT - 1) / kHT) * B;
       sm = sm && t64 <= (int64_t)small * 512;
     }
