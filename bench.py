@@ -426,9 +426,10 @@ def main():
     step_end = [ev0.elapsed_time(e) for e in step_ev]
     step_detail = {"end_ms": [round(x, 4) for x in step_end],
                    "first_step_ms": round(step_end[0], 4) if step_end else None,
-                   "steady_ms_per_step": (round((step_end[-1] - step_end[len(step_end) // 2]) /
-                                                max(1, len(step_end) - 1 - len(step_end) // 2), 4)
-                                          if len(step_end) > 2 else None),
+                   # period between the first and the second-to-last step ends: the last step
+                   # ends early (its batch runs alone once the other lane has drained)
+                   "steady_ms_per_step": (round((step_end[-2] - step_end[0]) / (len(step_end) - 2), 4)
+                                          if len(step_end) > 3 else None),
                    "host_submit_ms": round(t_sub * 1e3, 3),
                    "host_step_submit_ms_max": round(max(host_ms), 3) if host_ms else None,
                    "host_step_submit_ms_median": round(float(np.median(host_ms)), 3) if host_ms else None}
