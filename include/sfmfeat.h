@@ -249,9 +249,14 @@ int32_t sfm_match_pairs_prepped_dev(sfm_ctx* ctx, const float* desc, const int32
  * aux stream, no fork/join); 0 = the two largest levels' selection and descriptors overlap
  * the later levels' Harris on the context's aux stream (default; SFMFEAT_SERIAL=1 flips the
  * default).  Each stream maps onto one of the HIP runtime's hardware queues, and streams
- * beyond GPU_MAX_HW_QUEUES share one, so a batch pipeline chooses how many it uses. */
+ * beyond GPU_MAX_HW_QUEUES share one, so a batch pipeline chooses how many it uses.
+ * sfm_ctx_set_priority: HIP stream priority of the context's two streams (lower = higher
+ * priority, hipDeviceGetStreamPriorityRange; default 0); only before either stream exists
+ * (SFM_EINVAL after).  BatchPipeline's SFMFEAT_LANE_PRIO=1 gives its first lane the higher
+ * priority (an A/B setting). */
 int32_t sfm_ctx_stream(sfm_ctx* ctx, void** stream);
 int32_t sfm_ctx_set_serial(sfm_ctx* ctx, int32_t serial);
+int32_t sfm_ctx_set_priority(sfm_ctx* ctx, int32_t priority);
 
 /* ---------------- batches in flight: the lane gate ----------------
  * Replaces no reference interface: the reference runs one pair per host thread

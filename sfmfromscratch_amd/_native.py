@@ -63,6 +63,7 @@ SIGNATURES = {
                                                      ctypes.c_int32, ctypes.c_float, _vp, _vp, _vp, _vp]),
     "sfm_ctx_stream": (ctypes.c_int32, [_vp, ctypes.POINTER(_vp)]),
     "sfm_ctx_set_serial": (ctypes.c_int32, [_vp, ctypes.c_int32]),
+    "sfm_ctx_set_priority": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "sfm_gate_create": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(_vp)]),
     "sfm_gate_destroy": (ctypes.c_int32, [_vp]),
     "sfm_ctx_set_gate": (ctypes.c_int32, [_vp, _vp]),
@@ -195,6 +196,10 @@ class Context:
         h = _vp()
         check(self.lib.sfm_ctx_stream(self.handle, ctypes.byref(h)), self.handle)
         return int(h.value or 0)
+
+    def set_priority(self, priority: int):
+        """HIP priority of the context's streams (lower = higher); before they exist."""
+        check(self.lib.sfm_ctx_set_priority(self.handle, int(priority)), self.handle)
 
     def set_serial(self, serial: bool):
         """Every extraction stage on the caller's stream (no aux-stream overlap)."""

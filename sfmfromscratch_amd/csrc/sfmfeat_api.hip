@@ -86,6 +86,7 @@ struct sfm_ctx {
   bool match_direct = false;  // SFMFEAT_MATCH_DIRECT=1: all-pairs exact VALU kernel (A/B checks)
   bool exact_select = false;
   bool serial = false;        // SFMFEAT_SERIAL=1: no aux-stream overlap (diagnostic timings)
+  int prio = 0;               // stream priority of both context streams (sfm_ctx_set_priority)
   // SFMFEAT_MATCH_BUDGET_MB: matcher per-pair workspace bound (4 GB: 1,575 pairs of 2,500 rows per
   // sub-launch at 256 admitted targets per row, configs[2]'s 4,096-pair calls in three)
   size_t match_budget = (size_t)4096 << 20;
@@ -161,7 +162,7 @@ int ensure(sfm_ctx* c, DevBuf& b, size_t bytes) {
 
 // the stream of the host-pointer calls, created on first use
 int host_stream(sfm_ctx* c, hipStream_t* out) {
-  if (!c->stream) HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  if (!c->stream) HIPCHK(c, hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, c->prio));
   *out = c->stream;
   return SFM_OK;
 }
@@ -360,7 +361,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   const int L_aux = c->serial ? 0 : std::min(L, 2);
   hipStream_t ax = nullptr;
   if (L_aux > 0) {
-    if (!c->aux) HIPCHK(c, hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));  // on first use
+    if (!c->aux) HIPCHK(c, hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, c->prio));  // on first use
     ax = c->aux;
     HIPCHK(c, hipEventRecord(c->ev[L], st));
     HIPCHK(c, hipStreamWaitEvent(ax, c->ev[L], 0));
@@ -1111,6 +1112,13 @@ int32_t sfm_match(sfm_ctx* c, const float* d1, int64_t n1, const float* d2, int6
 int32_t sfm_ctx_set_serial(sfm_ctx* c, int32_t serial) {
   if (!c) return SFM_EINVAL;
   c->serial = serial != 0;
+  return SFM_OK;
+}
+
+int32_t sfm_ctx_set_priority(sfm_ctx* c, int32_t priority) {
+  if (!c) return SFM_EINVAL;
+  if (c->stream || c->aux) return set_err(c, SFM_EINVAL, "stream priority after the context's streams exist");
+  c->prio = priority;
   return SFM_OK;
 }
 
