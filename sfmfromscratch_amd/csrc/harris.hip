@@ -417,10 +417,13 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     const bool grad_in = tx0 - GA >= 0 && tx0 - GA + PWP <= W && ty0 - GA >= 0 && ty0 - GA + PH <= H;
     if (grad_in) sobel(std::false_type{});
     else sobel(std::true_type{});
-    if constexpr (TH == 64) {
+    __syncthreads();
+    if constexpr (F == 0) {
       // fused pyramid: the tile's 8 x 8 blocks of this level -> the next three exact 2x levels
       // (pyramid.hip k_down2x3's arithmetic, so the levels are bit-identical), one block per
-      // lane of the first wave, read from the image tile in LDS instead of from HBM again
+      // lane of the first wave, read from the image tile in LDS instead of from HBM again.
+      // After the Sobel barrier, so the other waves start their windows meanwhile (form 0
+      // keeps the image tile intact until the next tile's copy)
       float* const d1 = lvs.l[li].down[0];
       if (d1 != nullptr && tid < 64) {
         const int bx = tid & 7, by = tid >> 3;
@@ -438,7 +441,6 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
         }
       }
     }
-    __syncthreads();
     if constexpr (PP) {
       // the image tile is dead: the three products of every gradient (NaiveSIFT.py:61-63, the
       // same IEEE products the window phase formed) into their planes
