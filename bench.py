@@ -89,6 +89,46 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# Switches whose results are wrong by design (timing ablations).  Only the diagnostic build of
+# the library (make ABLATIONS=1) reads them at all; bench.py refuses to run with any of them
+# set unless --ablation-run marks the line as a diagnostic, not a measurement.
+ABLATION_SWITCHES = ("SFMFEAT_SKIP", "SFMFEAT_NMS_DRY")
+ENV_PREFIXES = ("SFMFEAT_", "SFM_", "HIP_", "GPU_", "HSA_", "ROCR_", "BENCH_", "NCCL_", "RCCL_")
+
+
+def ablation_switches_set(environ=None) -> list:
+    """Names of the results-wrong-by-design switches present in the environment."""
+    environ = os.environ if environ is None else environ
+    return sorted(k for k in environ if k in ABLATION_SWITCHES or (k.startswith("SFMFEAT_") and k.endswith("_ABL")))
+
+
+def bench_env(environ=None) -> dict:
+    """Every SFMFEAT_* / SFM_* / HIP_* / GPU_* / HSA_* / ROCR_* / BENCH_* / NCCL_* / RCCL_* variable
+    set for this run (recorded in the JSON line, so an A/B switch is visible in the result)."""
+    environ = os.environ if environ is None else environ
+    return {k: environ[k] for k in sorted(environ) if k.startswith(ENV_PREFIXES)}
+
+
+def emit(out: dict, args) -> None:
+    """Print the one JSON line with its provenance: the environment's switches, the library
+    and its build flags; a diagnostic (--ablation-run) line says so in its metric."""
+    from sfmfromscratch_amd import _native
+    out["env"] = bench_env()
+    out["library"] = _native.library_info()
+    out["ablation_run"] = bool(args.ablation_run)
+    if args.ablation_run:
+        out["metric"] = "DIAGNOSTIC ablation run, not a measurement: " + out["metric"]
+    print(json.dumps(out), flush=True)
+
+
+def default_workload(world: int) -> str:
+    """The workload `--gpus N` resolves to without --workload: BASELINE configs[1] (`c2`, 32
+    frames per GPU) on one GPU, configs[3] (`c4`, 2,048 frames in all, strong scaling) on N > 1.
+    The N > 1 line carries its own same-workload N = 1 figure (scaling_detail.t1_*), which is
+    the reference point of its efficiency — not the c2 line."""
+    return "c2" if world == 1 else "c4"
+
+
 def cpu_threads() -> int:
     """Host cores this process may use (the GPU box's share is 16; os.cpu_count() there
     reports the whole machine)."""
@@ -192,11 +232,22 @@ def main():
                          "FeatureRunner's ingest on the device (PIL BICUBIC x0.5 + _rgb2gray, Runner.py:33-46)")
     ap.add_argument("--inflight", type=int, default=int(os.environ.get("BENCH_INFLIGHT", "2")),
                     help="batches in flight (double-buffered contexts / slot tables, pipeline.BatchPipeline)")
+    ap.add_argument("--ablation-run", action="store_true",
+                    help="allow the timing-ablation switches (" + ", ".join(ABLATION_SWITCHES) + ", SFMFEAT_*_ABL; "
+                         "diagnostic library only): the line is then marked as a diagnostic, not a measurement")
+    ap.add_argument("--same-batch", action="store_true",
+                    help="c2: submit the same 32 frames every step (default: two distinct batches alternate, so "
+                         "no step re-reads the frames of the step before it)")
     ap.add_argument("--verify", action="store_true",
                     help="c4: after the timed run, re-extract a sample of frames and re-match a sample of this "
                          "rank's pairs with the plain (unchunked) calls and require bit-equal results")
     args = ap.parse_args()
 
+    abl = ablation_switches_set()
+    if abl and not args.ablation_run:
+        log(f"bench.py: refusing to measure with timing-ablation switches set ({', '.join(abl)}): their results "
+            "are wrong by design (pass --ablation-run for a diagnostic line)")
+        sys.exit(3)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
@@ -205,7 +256,7 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if args.workload is None:
-        args.workload = "c2" if world == 1 else "c4"
+        args.workload = default_workload(world)
 
     import torch
     import torch.distributed as dist
@@ -246,15 +297,23 @@ def main():
     B = args.batch
     # device-resident float32 frames of this rank's shard of the global sequence
     rgb = None
+    batches = None
     if args.rgb_ingest:  # decoded RGB at twice the size; the gray frames are made on the device
         uniq = [synth.make_frame_rgb_u8(2 * H, 2 * W, 1234, rank * B + i) for i in range(min(B, 8))]
         rgb = torch.from_numpy(np.stack([uniq[i % len(uniq)] for i in range(B)])).to(dev)
         del uniq
         frames = torch.empty((B, H, W), dtype=torch.float32, device=dev)
     else:
-        frames_u8 = np.stack([synth.make_frame_u8(H, W, 1234, rank * B + i) for i in range(B)])
-        frames = torch.from_numpy(synth.u8_to_gray(frames_u8)).to(dev)
-        del frames_u8
+        # two distinct batches (frames [2rB, 2rB + B) and [2rB + B, 2rB + 2B) of the global
+        # sequence) alternate step by step, so no step re-reads the frames the step before it
+        # read (one batch is 265 MB, the Infinity Cache 256 MB); --same-batch for the A/B
+        nb = 1 if args.same_batch else 2
+        batches = []
+        for j in range(nb):
+            frames_u8 = np.stack([synth.make_frame_u8(H, W, 1234, (rank * nb + j) * B + i) for i in range(B)])
+            batches.append(torch.from_numpy(synth.u8_to_gray(frames_u8)).to(dev))
+            del frames_u8
+        frames = batches[0]
     pairs_np = D.local_consecutive_pairs(B, rank, world)
     pairs = torch.from_numpy(pairs_np).to(dev)
     P = pairs.shape[0]
@@ -278,15 +337,17 @@ def main():
                 pipe.submit(f, hook=halo)
     else:
         def step():
-            pipe.submit(frames, hook=halo)
+            pipe.submit(batches[pipe.n % len(batches)] if not same_batch[0] else frames, hook=halo)
+    same_batch = [False]  # set for the same-batch comparison pass after the timed region
 
     def stage_work(counts, nsteps):
         """Algorithmic work of `nsteps` steps per stage:
         (bound, amount, unit, peak, algorithmic HBM bytes or None).  Latency-bound stages
-        (describe, top-k, median) get no roofline."""
+        (describe, top-k, median) get no roofline.  `counts`: each lane's slot counts (the
+        lanes take the steps in turn, and with alternating batches each lane its own batch)."""
         levels = [(H >> l, W >> l) for l in range(P_OCT["pyramid_level"])]
         px = sum(h * w for h, w in levels) * B * nsteps
-        pair_elems = sum(int(counts[i]) * int(counts[j]) for i, j in pairs_np) * 128 * nsteps
+        pair_elems = float(np.mean([sum(int(c[i]) * int(c[j]) for i, j in pairs_np) for c in counts])) * 128 * nsteps
         # k_down2x3 reads level 0 once and writes levels 1..3 (one launch); a 5th level is
         # one k_down2 from level 3.  Levels 1..3 exact 2x (H, W multiples of 8): the level-0
         # k_harris launch writes them from its image tiles (sfmfeat_api.hip, SFMFEAT_PYR_FUSED),
@@ -343,7 +404,7 @@ def main():
         return tot
 
     def lane_counts():
-        return pipe.lanes[0]["slots"].count.cpu().numpy()
+        return [ln["slots"].count.cpu().numpy() for ln in pipe.lanes]
 
     # Per-stage device times (every stage bracketed by HIP events) in an untimed pass with
     # one batch on the GPU at a time; it names the dominant stage, whose events alone
@@ -396,6 +457,7 @@ def main():
 
     # W warm-up steps: the same two-lane pipeline as the timed steps, right before them
     run_steps(args.warmup)
+    pipe.n = 0  # the timed steps start on lane 0 with the first batch
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -463,8 +525,34 @@ def main():
         torch.cuda.synchronize()
         prof = prof_read()
         prof_enable(False)
-    counts = lane_counts()
-    nmatch = pipe.lanes[0]["mout"][2].cpu().numpy()
+    # the same K steps again with one batch submitted every step (the pre-round-5 workload): the
+    # line reports its rate beside `value` (alternating batches) as the cost of never re-reading
+    # the previous step's frames
+    same_value = None
+    if batches is not None and len(batches) > 1:
+        same_batch[0] = True
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        pipe.n = 0
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ts = time.perf_counter()
+        s0.record()
+        run_steps(args.steps)
+        s1.record()
+        spin_until(s1)
+        torch.cuda.synchronize()
+        el = max(time.perf_counter() - ts, s0.elapsed_time(s1) / 1e3)
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        same_value = world * B * args.steps / el
+        same_batch[0] = False
+
+    counts_l = lane_counts()
+    counts = np.concatenate(counts_l) if len(counts_l) > 1 and batches is not None and len(batches) > 1 else counts_l[0]
+    nmatch = np.concatenate([ln["mout"][2].cpu().numpy() for ln in pipe.lanes])
 
     images = world * B * args.steps
     value = images / elapsed
@@ -476,7 +564,7 @@ def main():
         if os.path.exists(TRAFFIC_FILE) and args.workload == "c2" and not args.rgb_ingest:
             with open(TRAFFIC_FILE) as f:
                 traffic = json.load(f).get("bytes_per_launch", {})
-        bound, amount, unit, peak, abytes = stage_work(counts, args.steps)[dom]
+        bound, amount, unit, peak, abytes = stage_work(counts_l, args.steps)[dom]
         ms, n = prof[dom]
         achieved = amount / (ms / 1e3)
         kname = KERNELS[dom]
@@ -525,15 +613,21 @@ def main():
                        (f"BASELINE configs[4] per-GPU share: {B}x 4K per step, ScaleRotInvSIFT 5-level x2 "
                         "octave pyramid, k=8000, fw 18, NNRatio 0.85 over consecutive pairs"),
                        "frames_per_gpu": B, "image": [H, W], "pairs_per_gpu": int(P),
-                       "keypoints_mean": float(np.mean(counts[:B])),
+                       "distinct_batches": len(batches) if batches is not None else 1,
+                       "keypoints_mean": float(np.mean([c[:B].mean() for c in counts_l])),
                        "matches_mean": float(np.mean(nmatch[nmatch >= 0])) if (nmatch >= 0).any() else 0.0,
                        "parallelism": f"image-shard x{world}", "batches_in_flight": args.inflight},
             "roofline": roof,
             "cpu_baseline": cpu,
             "stages_ms": stages,
             "steps_detail": step_detail,
+            "batches_detail": ({"distinct_batches": len(batches), "alternation": "step i submits batch i % 2 "
+                                "(frames [2rB, 2rB+B) / [2rB+B, 2rB+2B)); lane i % 2 runs it",
+                                "value_same_batch_every_step": round(same_value, 2),
+                                "delta_pct_vs_same_batch": round(100.0 * (value - same_value) / same_value, 2)}
+                               if same_value else None),
         }
-        print(json.dumps(out), flush=True)
+        emit(out, args)
     if world > 1:
         dist.destroy_process_group()
 
@@ -606,7 +700,7 @@ def run_all_pairs(args, torch, dev):
     elems = int(sum(counts[i] * counts[j] for i, j in pairs_np)) * 128 * args.steps
     ms, n = prof.get("match", (0.0, 0))
     ach = MATCH_FLOP_PER_ELEM * elems / 1e12 / (ms / 1e3) if ms else None
-    print(json.dumps({
+    emit({
         "metric": "images/sec detect+describe+match, 1080p, all pairs (BASELINE configs[2])",
         "value": round(N * args.steps / elapsed, 3), "unit": "images/sec", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -623,7 +717,7 @@ def run_all_pairs(args, torch, dev):
                      "avg_launch_ms": round(ms / max(n, 1), 4), "launches": n,
                      "note": "GEMM-equivalent 2*n1*n2*128 flop per pair (SURVEY.md §8d) against the split-f16 "
                              "MFMA bound 2500/3 TFLOP/s"},
-        "cpu_baseline": None}), flush=True)
+        "cpu_baseline": None}, args)
 
 
 XGMI_LINK_GBS = 153.0  # per xGMI link per direction (task spec); the 8-GPU node is a full mesh
@@ -781,14 +875,17 @@ def run_gather(args, torch, dist, dev, rank, world):
     eff = None
     if t1 is not None:
         eff = {"efficiency": round(t1 / (world * tn), 4), "t1_ms": round(t1 * 1e3, 3), "tn_ms": round(tn * 1e3, 3),
-               "definition": "T1 / (N * TN): T1 = the same job alone on rank 0's GPU (no exchange)"}
+               "t1_images_per_s": round(n_global / t1, 2), "tn_images_per_s": round(n_global / tn, 2),
+               "definition": "T1 / (N * TN): T1 = the same job alone on rank 0's GPU (no exchange)",
+               "note": "the N = 1 reference of this line is t1_images_per_s (the same configs[3] job on one GPU), "
+                       "not the N = 1 headline line (configs[1], 32 frames per step)"}
     if comm is not None and t_compute is not None:
         comm["compute_only_ms"] = round(t_compute * 1e3, 3)
         if t_alone:
             comm["hidden_fraction"] = round(min(1.0, max(0.0, 1.0 - (tn - t_compute) / t_alone)), 4)
             comm["hidden_note"] = "1 - (TN - T_compute) / T_gather_alone; T_compute = the job with collectives skipped"
     if rank == 0:
-        print(json.dumps({
+        emit({
             "metric": "images/sec detect+describe+match, 1080p, 1/2/4/8 MI355X",
             "value": round(n_global / tn, 2), "unit": "images/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(tn * 1e3, 3),
@@ -807,7 +904,7 @@ def run_gather(args, torch, dist, dev, rank, world):
             "scaling_detail": eff,
             "collective": comm,
             "roofline": roof,
-            "cpu_baseline": None}), flush=True)
+            "cpu_baseline": None}, args)
     if world > 1:
         dist.destroy_process_group()
 

@@ -82,6 +82,13 @@ void sfm_params_default(sfm_params* p, int32_t mode);
 /* ABI version, bumped on any signature change. */
 int32_t sfm_abi_version(void);
 
+/* Build flags of this library: SFM_BUILD_ABLATIONS set only in the diagnostic build
+ * (make ABLATIONS=1), whose timing switches (SFMFEAT_SKIP, SFMFEAT_*_ABL, SFMFEAT_NMS_DRY) skip
+ * or hollow out work by design; the shipped build reads none of them.  (No reference
+ * counterpart: build provenance for bench lines.) */
+#define SFM_BUILD_ABLATIONS 1
+int32_t sfm_build_flags(void);
+
 /* Maximum number of keypoints one image can produce:
  * ScaleRot: pyramid_level * int(k / pyramid_level)  (ScaleRotInvSIFT.py:90 scaled_k)
  * Naive:    k                                       (NaiveSIFT.py:100-103) */

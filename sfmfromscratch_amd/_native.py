@@ -31,6 +31,7 @@ _vp = ctypes.c_void_p
 SIGNATURES = {
     "sfm_params_default": (None, [ctypes.POINTER(SfmParams), ctypes.c_int32]),
     "sfm_abi_version": (ctypes.c_int32, []),
+    "sfm_build_flags": (ctypes.c_int32, []),
     "sfm_keypoint_capacity": (ctypes.c_int64, [ctypes.POINTER(SfmParams)]),
     "sfm_pyramid_dims": (ctypes.c_int32, [ctypes.POINTER(SfmParams), ctypes.c_int32, ctypes.c_int32, _i32p]),
     "sfm_ctx_create": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(SfmParams), ctypes.POINTER(_vp)]),
@@ -130,6 +131,18 @@ def load_library(path: str | None = None):
         if path is None:
             _lib = L
         return L
+
+
+SFM_BUILD_ABLATIONS = 1  # include/sfmfeat.h
+
+
+def library_info() -> dict:
+    """Path and build flags of the loaded library (bench lines record them): `ablations` is
+    True only for the diagnostic build (make ABLATIONS=1), whose timing switches skip work."""
+    L = load_library()
+    flags = int(L.sfm_build_flags())
+    return {"path": os.path.relpath(LIB_PATH, os.path.dirname(_HERE)) if os.path.isabs(LIB_PATH) else LIB_PATH,
+            "build_flags": flags, "ablations": bool(flags & SFM_BUILD_ABLATIONS)}
 
 
 def check(rc: int, ctx=None):

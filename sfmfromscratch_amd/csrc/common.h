@@ -11,6 +11,17 @@
 
 #define SFM_DEV __device__ __forceinline__
 
+// Timing ablations (results wrong by design: SFMFEAT_SKIP, SFMFEAT_HARRIS_ABL,
+// SFMFEAT_SELECT_ABL, SFMFEAT_DQ_ABL, SFMFEAT_NMS_DRY) exist only in a diagnostic build of the
+// library (make ABLATIONS=1: -DSFM_ABLATIONS, its own output directory).  The shipped
+// libsfmfeat.so never reads those switches, so no environment can make it skip work;
+// sfm_build_flags() tells the two builds apart.
+#ifdef SFM_ABLATIONS
+#define SFM_ABLATION_ENV(name) getenv(name)
+#else
+#define SFM_ABLATION_ENV(name) ((const char*)nullptr)
+#endif
+
 namespace sfm {
 
 constexpr int kWave = 64;

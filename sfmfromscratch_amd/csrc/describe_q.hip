@@ -627,7 +627,7 @@ bool launch_describe_quad(const float* lvl, int B, int H, int W, int fw, int rot
     case 18:
       if (rotate) {
         static const int abl = [] {
-          const char* v = getenv("SFMFEAT_DQ_ABL");
+          const char* v = SFM_ABLATION_ENV("SFMFEAT_DQ_ABL");
           return v ? atoi(v) : 0;
         }();
         switch (abl) {

@@ -803,7 +803,7 @@ void launch_harris_levels(const HarrisLevels& g, int B, const float* d_gauss, in
     case 7: {
       // SFMFEAT_HARRIS_ABL=1|2: timing ablations inside the pipeline (results are wrong)
       static const int abl = [] {
-        const char* e = getenv("SFMFEAT_HARRIS_ABL");
+        const char* e = SFM_ABLATION_ENV("SFMFEAT_HARRIS_ABL");
         return e ? atoi(e) : 0;
       }();
       if (abl == 1) launch_ks<7, 1>(g, B, d_gauss, alpha, st);

@@ -511,7 +511,7 @@ static void launch_tile(const float* R, const MedianState* state, uint64_t* cand
     // SFMFEAT_NMS_SH=8: 8-row strips (A/B); SFMFEAT_NMS_DRY=1: a candidate-free read pass
     // of R ahead of the real one (timing only: how fast R reads once Harris's writes drained)
     static const int sh = [] { const char* e = getenv("SFMFEAT_NMS_SH"); return e ? atoi(e) : kStreamSH; }();
-    static const bool dry = [] { const char* e = getenv("SFMFEAT_NMS_DRY"); return e && atoi(e) != 0; }();
+    static const bool dry = [] { const char* e = SFM_ABLATION_ENV("SFMFEAT_NMS_DRY"); return e && atoi(e) != 0; }();
     static const int band = [] { const char* e = getenv("SFMFEAT_NMS_BAND"); return e ? atoi(e) : kBandStrips; }();
     if (band >= 1 && band <= 4 && !dry) {
       const int rows = 8 * band;

@@ -551,7 +551,7 @@ size_t topk_lds_bytes() {
 void launch_select_levels(const SelectLevels& g, int kcap, int k, int B, int ksize, hipStream_t st) {
   if (g.n < 1 || g.n > kSelectMaxLevels || B < 1) return;
   static const int abl = [] {
-    const char* e = getenv("SFMFEAT_SELECT_ABL");
+    const char* e = SFM_ABLATION_ENV("SFMFEAT_SELECT_ABL");
     return e ? atoi(e) : 0;
   }();
   hipLaunchKernelGGL(k_select, dim3(B * g.n), dim3(1024), topk_lds_bytes(), st, g, kcap, k, ksize / 2, B, abl);

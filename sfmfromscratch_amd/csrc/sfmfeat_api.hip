@@ -94,9 +94,9 @@ struct sfm_ctx {
   int last_H = 0, last_W = 0;
   // stage profiling (sfm_profile_*): HIP events bracketing each stage's launches
   bool prof = false;
-  uint32_t prof_mask = ~0u;
+  uint32_t prof_mask = ~0u;  // stages bracketed while profiling (sfm_profile_stages)
   int64_t extractions = 0;  // extract_impl calls (SFMFEAT_SKIP leaves the first one whole)
-  int64_t match_calls = 0;  // match sub-launches (likewise)  // stages bracketed while profiling (sfm_profile_stages)
+  int64_t match_calls = 0;  // match sub-launches (likewise)
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> prof_pending;
   std::vector<hipEvent_t> prof_pool;
   double prof_ms[SFM_PROF_STAGES] = {0};
@@ -269,7 +269,7 @@ int reserve_impl(sfm_ctx* c, int B, int H, int W) {
 // 16 Harris of the levels above 0
 int skip_mask() {
   static const int m = [] {
-    const char* e = getenv("SFMFEAT_SKIP");
+    const char* e = SFM_ABLATION_ENV("SFMFEAT_SKIP");
     return e ? atoi(e) : 0;
   }();
   return m;
@@ -343,6 +343,9 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   if (!zeroed || fill_launches) {
     HIPCHK(c, hipMemsetAsync(c->d_hist.p, 0, hist_bytes, st));
     HIPCHK(c, hipMemsetAsync(c->d_counts.p, 0, count_bytes, st));
+    // the fused pyramid's later k_down2x3 (pyramid_from(4), after level 0's Harris) must not
+    // zero them again: level 0's histogram and counters are live by then
+    zeroed = true;
   }
   unsigned long long* medcnt = as<unsigned long long>(c->d_counts);
   unsigned long long* candcnt = medcnt + (size_t)L * B * kCounterStride;    // certified NMS
@@ -646,6 +649,14 @@ void sfm_params_default(sfm_params* p, int32_t mode) {
 }
 
 int32_t sfm_abi_version(void) { return 1; }
+
+int32_t sfm_build_flags(void) {
+#ifdef SFM_ABLATIONS
+  return SFM_BUILD_ABLATIONS;
+#else
+  return 0;
+#endif
+}
 
 int64_t sfm_keypoint_capacity(const sfm_params* p) {
   if (!p) return 0;

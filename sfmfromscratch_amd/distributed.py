@@ -402,7 +402,13 @@ class ChunkedGatherJob:
         if compact is None:
             compact = os.environ.get("SFM_GATHER_COMPACT", "1") != "0"
         self.compact = bool(compact) and world > 1 and not self.halo
-        self.stage = CompactStage(torch, world, Bx, cap, dev) if self.compact else None
+        # one staging area per lane: chunk c's rows are packed, gathered and unpacked on lane
+        # c % inflight's stream, and nothing orders two lanes' streams against each other, so
+        # a shared stage would let chunk c+1's send copy overwrite chunk c's buffer while
+        # chunk c's gather still reads it (and its gather land in the receive buffer chunk c
+        # is being unpacked from)
+        for ln in self.lanes:
+            ln["stage"] = CompactStage(torch, world, Bx, cap, dev) if self.compact else None
         self.gathered_rows = []  # per chunk of the last run: M (compact) or cap
         self.CH = 4096  # 'all': pairs per matcher launch
         self.keep_all_results = bool(keep_all_results)
@@ -493,7 +499,7 @@ class ChunkedGatherJob:
                 for w in cworks:
                     w.wait()
                 M = int(self.table.count[base:base + world * bc].max().item()) if bc else 0
-                works, _ = allgather_chunk_rows(dist, self.table, plan, c, ln["slots"], self.stage, M,
+                works, _ = allgather_chunk_rows(dist, self.table, plan, c, ln["slots"], ln["stage"], M,
                                                 group=self.group, coalesce=self.coalesce)
                 ln["pending"] = works
                 done = torch.cuda.Event()
@@ -579,7 +585,7 @@ class ChunkedGatherJob:
         each chunk's M, rows, unpack; else full-capacity slots), on lane 0's last slots."""
         import time
         torch, dist, plan = self.torch, self.dist, self.plan
-        src = self.lanes[0]["slots"]
+        src, stage = self.lanes[0]["slots"], self.lanes[0]["stage"]
         dist.barrier(group=self.group)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -590,7 +596,7 @@ class ChunkedGatherJob:
                         w.wait()
                     bc, base = plan.chunk_size(c), plan.chunk_base(c)
                     M = int(self.table.count[base:base + plan.world * bc].max().item())
-                    allgather_chunk_rows(dist, self.table, plan, c, src, self.stage, M, group=self.group,
+                    allgather_chunk_rows(dist, self.table, plan, c, src, stage, M, group=self.group,
                                          coalesce=self.coalesce)
                 else:
                     for w in self.gather_chunk(c, src):

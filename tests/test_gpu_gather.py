@@ -114,6 +114,9 @@ def _rank_worker(rank, world, port, pairs, errq):
         plan = D.GatherPlan(16, world, 3, pairs)  # S = 8 per rank: chunks of 3, 3, 2
         job = D.ChunkedGatherJob(PP, RATIO, plan, rank, H, W, dist=dist, inflight=2)
         assert not job.coalesce  # gloo: one collective per field
+        # the count-compacted gather stages each lane's rows in that lane's own buffers (the
+        # lanes' streams are not ordered against each other)
+        assert job.compact and len({id(ln["stage"]) for ln in job.lanes}) == len(job.lanes) == 2
         frames = _frames(torch, plan, rank)
         job.run(frames, record_sent=True)
         torch.cuda.synchronize()

@@ -436,3 +436,24 @@ def test_match_workspace_budget_sub_launches_equal_one_launch(monkeypatch):
     for a, b, c in zip(ref, got, got2):
         assert torch.equal(a, b) and torch.equal(a, c)
 
+
+
+def test_seven_levels_fused_pyramid_then_down2x3_vs_oracle():
+    """L = 7 at a size that is a multiple of 64: levels 1-3 come from the level-0 Harris launch
+    and levels 4-6 from a k_down2x3 pass after it.  That pass must not zero the histograms and
+    counters level 0's Harris has already written (the fill launches did).  Keypoints and
+    descriptors of both frames bit-identical to the oracle."""
+    torch = pytest.importorskip("torch")
+    from sfmfromscratch_amd.pipeline import BatchExtractor
+    H, W = 512, 1024
+    pp = dict(P_OCT, num_interest_points=1400, pyramid_level=7)
+    u8 = synth.make_batch_u8(2, H, W, seed=77)
+    s = BatchExtractor(pp).extract(torch.from_numpy(u8).cuda())
+    torch.cuda.synchronize()
+    counts, xy, desc = s.count.cpu().numpy(), s.xy.cpu().numpy(), s.desc.cpu().numpy()
+    for i in range(2):
+        OX, OY, OD, _ = O.extract(synth.u8_to_gray(u8[i]), pp)
+        n = counts[i]
+        assert n == len(OX) and n > 500
+        assert np.array_equal(xy[i, :n, 0], OX) and np.array_equal(xy[i, :n, 1], OY)
+        assert np.array_equal(bits(desc[i, :n]), bits(OD))

@@ -1,13 +1,14 @@
 #!/bin/bash
 # Describe timing ablations (SFMFEAT_DQ_ABL, describe_q.hip): kernel trace per variant.
+# (timing ablations: needs the diagnostic library, `make -C sfmfromscratch_amd/csrc ABLATIONS=1`)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
 for A in ${ABLS:-0 1 2 4 8 7 16 32 64 55 127}; do
-  SFMFEAT_SERIAL=1 SFMFEAT_DQ_ABL=$A timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/dqabl_$A -o run -- \
-    python bench.py --steps 3 --warmup 1 --cpu-sample 0 --no-profile > $OUT/dqabl_$A.log 2>&1 || exit 1
+  SFMFEAT_LIB=$PWD/sfmfromscratch_amd/lib_diag/libsfmfeat.so SFMFEAT_SERIAL=1 SFMFEAT_DQ_ABL=$A timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/dqabl_$A -o run -- \
+    python bench.py --steps 3 --warmup 1 --cpu-sample 0 --no-profile --ablation-run > $OUT/dqabl_$A.log 2>&1 || exit 1
   python - "$A" <<'PY'
 import csv, glob, sys
 a = sys.argv[1]

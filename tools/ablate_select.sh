@@ -1,13 +1,14 @@
 #!/bin/bash
 # k_select timing ablations (SFMFEAT_SELECT_ABL, select.hip; results wrong by design): kernel
+# (timing ablations: needs the diagnostic library, `make -C sfmfromscratch_amd/csrc ABLATIONS=1`)
 # trace of a serial bench run per variant, mean / min duration per launch shape.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 for A in ${ABLS:-0 1 2 3}; do
-  SFMFEAT_SERIAL=1 SFMFEAT_SELECT_MERGE=0 SFMFEAT_SELECT_ABL=$A timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/selabl_$A -o run -- \
-    python bench.py --steps 3 --warmup 1 --cpu-sample 0 --no-profile ${BENCH_ARGS:-} > gpurun_out/selabl_$A.log 2>&1 || exit 1
+  SFMFEAT_LIB=$PWD/sfmfromscratch_amd/lib_diag/libsfmfeat.so SFMFEAT_SERIAL=1 SFMFEAT_SELECT_MERGE=0 SFMFEAT_SELECT_ABL=$A timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/selabl_$A -o run -- \
+    python bench.py --steps 3 --warmup 1 --cpu-sample 0 --no-profile --ablation-run ${BENCH_ARGS:-} > gpurun_out/selabl_$A.log 2>&1 || exit 1
   python - "$A" "${LEVELS:-4}" <<'PY'
 import csv, glob, sys
 a = sys.argv[1]

@@ -1,0 +1,125 @@
+// Diagnostic: issue cost of the packed-FP32 forms a window sum can use on gfx950, at 1..4
+// waves per SIMD.  Each wave runs ITERS x 16 independent fmas into 16 accumulators with
+// distinct operand registers (8 tap pairs, 8 value pairs), so the cost is the instruction's
+// own, not a dependency chain's.  Forms:
+//   0 v_pk_fma_f32, no op_sel (both halves from their own half: a pre-paired layout)
+//   1 v_pk_fma_f32 op_sel_hi:[1,0,1]      src1 low half to both results (k_harris H = 0)
+//   2 v_pk_fma_f32 op_sel:[1,0,0]         src0 high half to both results (k_harris H = 1)
+//   3 v_pk_fma_f32 op_sel_hi:[0,1,1]      src0 low half to both results (a broadcast tap)
+//   4 v_fmac_f32                          scalar
+//   5 v_pk_mul_f32, no op_sel
+//   6 v_pk_add_f32, no op_sel
+//   7 v_pk_fma_f32 plain with 8 independent accumulators only (the dependency distance of a row pair)
+// Usage: pk_rate [iters]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int MODE>
+__global__ void __launch_bounds__(256) k_rate(float* out, int iters, float s, unsigned long long* cyc) {
+  f32x2 a[16];
+  float b[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    a[i] = f32x2{s * i, s + i};
+    b[i] = s * (i + 1);
+  }
+  f32x2 kp[8], vp[8];
+  float kv[8], vv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    kp[i] = f32x2{s * (0.5f + i), s * (0.25f + i)};
+    vp[i] = f32x2{s * i, s - i};
+    kv[i] = s * (0.75f + i);
+    vv[i] = s * (1.5f - i);
+  }
+  __syncthreads();
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if constexpr (MODE == 0)
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(a[i]) : "v"(kp[i & 7]), "v"(vp[(i + 3) & 7]));
+      else if constexpr (MODE == 1)
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(a[i]) : "v"(kp[i & 7]), "v"(vp[(i + 3) & 7]));
+      else if constexpr (MODE == 2)
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(a[i]) : "v"(vp[(i + 3) & 7]), "v"(kp[i & 7]));
+      else if constexpr (MODE == 3)
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(a[i]) : "v"(kp[i & 7]), "v"(vp[(i + 3) & 7]));
+      else if constexpr (MODE == 4)
+        asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(b[i]) : "v"(kv[i & 7]), "v"(vv[(i + 3) & 7]));
+      else if constexpr (MODE == 5)
+        asm volatile("v_pk_mul_f32 %0, %1, %2" : "+v"(a[i]) : "v"(kp[i & 7]), "v"(vp[(i + 3) & 7]));
+      else if constexpr (MODE == 6)
+        asm volatile("v_pk_add_f32 %0, %1, %2" : "+v"(a[i]) : "v"(kp[i & 7]), "v"(vp[(i + 3) & 7]));
+      else
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(a[i & 7]) : "v"(kp[i & 7]), "v"(vp[(i + 3) & 7]));
+    }
+  }
+  const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+  float acc = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc += a[i].x + a[i].y + b[i];
+  if (acc == 1.2345f) out[0] = acc;
+  const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+  if ((threadIdx.x & 63) == 0) {
+    cyc[2 * (blockIdx.x * 4 + (threadIdx.x >> 6))] = c1 - c0;
+    cyc[2 * (blockIdx.x * 4 + (threadIdx.x >> 6)) + 1] = hw;
+  }
+}
+
+template <int MODE>
+static void launch(dim3 grid, float* out, int iters, unsigned long long* cyc) {
+  hipLaunchKernelGGL(k_rate<MODE>, grid, dim3(256), 0, 0, out, iters, 1.0f, cyc);
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 20000;
+  float* out;
+  (void)hipMalloc(&out, 4);
+  unsigned long long* cyc;
+  (void)hipMalloc(&cyc, 8 * 65536);
+  static unsigned long long hc[65536];
+  hipDeviceProp_t p;
+  (void)hipGetDeviceProperties(&p, 0);
+  const int cus = p.multiProcessorCount;
+  const char* names[8] = {"pk_fma plain", "pk_fma src1.lo bcast", "pk_fma src0.hi bcast", "pk_fma src0.lo bcast",
+                          "fmac_f32", "pk_mul plain", "pk_add plain", "pk_fma plain 8 accs"};
+  void (*fns[8])(dim3, float*, int, unsigned long long*) = {launch<0>, launch<1>, launch<2>, launch<3>,
+                                                            launch<4>, launch<5>, launch<6>, launch<7>};
+  for (int mode = 0; mode < 8; ++mode)
+    for (int wps = 1; wps <= 4; ++wps) {
+      dim3 grid(cus * wps);
+      fns[mode](grid, out, iters, cyc);
+      (void)hipDeviceSynchronize();
+      hipEvent_t e0, e1;
+      (void)hipEventCreate(&e0);
+      (void)hipEventCreate(&e1);
+      (void)hipEventRecord(e0, 0);
+      fns[mode](grid, out, iters, cyc);
+      (void)hipEventRecord(e1, 0);
+      (void)hipEventSynchronize(e1);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      (void)hipMemcpy(hc, cyc, 8 * 2 * 4 * grid.x, hipMemcpyDeviceToHost);
+      static int occ[1 << 16];
+      for (int i = 0; i < (1 << 16); ++i) occ[i] = 0;
+      int maxocc = 0;
+      double mc = 0, sc = 0;
+      for (unsigned w = 0; w < 4 * grid.x; ++w) {
+        mc = hc[2 * w] > mc ? hc[2 * w] : mc;
+        sc += hc[2 * w];
+        const unsigned key = ((unsigned)hc[2 * w + 1] >> 4) & 0xfff3u;
+        maxocc = ++occ[key] > maxocc ? occ[key] : maxocc;
+      }
+      const double mean = sc / (4 * grid.x);
+      printf("%-26s waves/SIMD %d: %.3f ms, cycles per instruction per SIMD %.2f (max wave) %.2f (mean wave), %.0f MHz\n",
+             names[mode], maxocc, ms, mc / ((double)iters * 16 * maxocc), mean / ((double)iters * 16 * maxocc),
+             mc / (ms * 1e-3) / 1e6);
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+    }
+  return 0;
+}
