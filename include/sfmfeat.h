@@ -260,7 +260,7 @@ int32_t sfm_match_pairs_prepped_dev(sfm_ctx* ctx, const float* desc, const int32
  * sfm_ctx_set_priority: HIP stream priority of the context's two streams (lower = higher
  * priority, hipDeviceGetStreamPriorityRange; default 0); only before either stream exists
  * (SFM_EINVAL after).  BatchPipeline's SFMFEAT_LANE_PRIO=1 gives its first lane the higher
- * priority (an A/B setting). */
+ * priority (an A/B setting; DESIGN_LOG.md §B). */
 int32_t sfm_ctx_stream(sfm_ctx* ctx, void** stream);
 int32_t sfm_ctx_set_serial(sfm_ctx* ctx, int32_t serial);
 int32_t sfm_ctx_set_priority(sfm_ctx* ctx, int32_t priority);

@@ -200,7 +200,7 @@ __global__ void __launch_bounds__(256) k_nms_tile(const float* __restrict__ R,
 // per row), the horizontal max3 takes its outer columns from the neighbouring lanes
 // (__shfl_up/__shfl_down; the wave's edge lanes load them), then the vertical max3 and the
 // predicate.  No LDS staging: the tiled kernel's per-tile barriers and LDS round trip
-// paced it at ~21 % of HBM.  Candidates are appended with one atomic per
+// paced it at ~21 % of HBM (DESIGN_LOG.md §B).  Candidates are appended with one atomic per
 // workgroup; their order is irrelevant (k_topk orders them by key).
 template <int SH, int NT>
 __global__ void __launch_bounds__(NT) k_nms_stream(const float* __restrict__ R,

@@ -160,7 +160,7 @@ class BatchPipeline:
         # host and aux streams — four with two lanes, one per hardware queue at the runtime's
         # default of four) or "torch" (a stream from torch's pool per lane, which shares
         # hardware queues with the contexts' aux streams by creation order: 35.05k vs 36.03k
-        # img/s over five interleaved driver-command runs each).  serial_lanes: lane indices whose
+        # img/s over five interleaved driver-command runs each, DESIGN_LOG.md §B).  serial_lanes: lane indices whose
         # extraction runs on one stream (sfm_ctx_set_serial), e.g. "0" in SFMFEAT_SERIAL_LANES
         if lane_streams is None:
             lane_streams = os.environ.get("SFMFEAT_LANE_STREAMS", "context")

@@ -77,6 +77,6 @@ def test_shipped_library_has_no_ablations():
         pytest.skip("libsfmfeat.so not built")
     assert _native.load_library(lib).sfm_build_flags() == 0
     data = open(lib, "rb").read()
-    for name in (b"SFMFEAT_SKIP", b"SFMFEAT_HARRIS_ABL", b"SFMFEAT_SELECT_ABL", b"SFMFEAT_DQ_ABL",
+    for name in (b"SFMFEAT_SKIP", b"SFMFEAT_HARRIS_ABL", b"SFMFEAT_SELECT_ABL", b"SFMFEAT_DQ_ABL", b"SFMFEAT_MATCH_ABL",
                  b"SFMFEAT_NMS_DRY"):
         assert name not in data, name

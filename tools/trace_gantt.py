@@ -1,9 +1,10 @@
 """Text timeline of a rocprofv3 kernel trace (diagnostic): the dispatches of a steady-state
-window (default: the 4th-last .. 2nd-last k_down2x3 starts, i.e. two pipelined steps), one line
+window (default: the 4th-last .. 2nd-last starts of the anchor kernel, k_match_compact: one per
+step, i.e. two pipelined steps), one line
 each — start offset, duration, queue/stream, kernel, grid — plus per-stream busy time and the
 time with no kernel running.
 
-usage: python tools/trace_gantt.py <trace dir or kernel_trace.csv> [first_step_from_end=4] [steps=2]"""
+usage: python tools/trace_gantt.py <trace dir or kernel_trace.csv> [first_step_from_end=4] [steps=2] [anchor]"""
 import csv
 import glob
 import sys
@@ -13,9 +14,10 @@ if not path.endswith(".csv"):
     path = sorted(glob.glob(f"{path}/**/*kernel_trace.csv", recursive=True))[0]
 back = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 nst = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+anchor = sys.argv[4] if len(sys.argv) > 4 else "k_match_compact"
 rows = list(csv.DictReader(open(path)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-firsts = [i for i, r in enumerate(rows) if "k_down2x3" in r["Kernel_Name"]]
+firsts = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
 a = firsts[-back]
 b = firsts[-back + nst] if -back + nst < 0 else len(rows)
 t0 = int(rows[a]["Start_Timestamp"])
