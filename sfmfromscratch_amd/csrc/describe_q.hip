@@ -625,6 +625,7 @@ bool launch_describe_quad(const float* lvl, int B, int H, int W, int fw, int rot
     SFM_DQ_CASE(14)
     SFM_DQ_CASE(16)
     case 18:
+#ifdef SFM_ABLATIONS  // timing ablations: the diagnostic build only
       if (rotate) {
         static const int abl = [] {
           const char* v = SFM_ABLATION_ENV("SFMFEAT_DQ_ABL");
@@ -650,6 +651,7 @@ bool launch_describe_quad(const float* lvl, int B, int H, int W, int fw, int rot
             break;
         }
       }
+#endif
       SFM_DQ_BODY(18)
     SFM_DQ_CASE(20)
     SFM_DQ_CASE(22)

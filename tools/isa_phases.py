@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""Per-phase VALU instruction counts of one k_harris<7,true,0,0> tile iteration, from the
+gfx950 disassembly of the built library (no GPU needed).
+
+The tile loop runs from its first s_barrier to the backward branch that closes it.  Phases:
+  sobel     the interior strip loop (edge tiles run the masked variant instead), weighted
+            by its trip count ceil(PH * NS / NT)
+  window    v_pk_fma_f32 / v_fmac_f32 / v_fma_f32 of the window sums (incl. the edge-row
+            scalar fmas the compiler sank into the epilogue)
+  products  v_pk_mul_f32 (Ix^2, Iy^2, IxIy per gradient row)
+  R         v_mul/v_sub/v_add f32 of det - alpha tr^2
+  hist      the digit-1 key and its LDS add (v_not/v_lshrrev/v_and, ds_add)
+  masks     v_cmp / v_cndmask (the image tile's zero border, the histogram's bounds)
+  other     addressing and moves (incl. the fused down2x3 block of wave 0, counted as if
+            every wave ran it: an upper bound)
+The phases are classified by opcode (the compiler interleaves R and the histogram with the
+window's last rows), so the table is per tile-wave, not a timeline.
+usage: tools/isa_phases.py [lib.so] [kernel-substring]"""
+import collections
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LLVM = "/opt/rocm/lib/llvm/bin"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def disassemble(lib):
+    with tempfile.TemporaryDirectory() as tmp:
+        fb = os.path.join(tmp, "fb.bin")
+        subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib, fb], check=True)
+        data = open(fb, "rb").read()
+        starts = [m.start() for m in re.finditer(re.escape(MAGIC), data)]
+        out = []
+        for n, i in enumerate(starts):
+            j = starts[n + 1] if n + 1 < len(starts) else len(data)
+            b, e = os.path.join(tmp, f"b{n}.bin"), os.path.join(tmp, f"b{n}.elf")
+            open(b, "wb").write(data[i:j])
+            subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={b}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={e}"], check=True)
+            out.append(subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--mcpu=gfx950", e],
+                                      check=True, capture_output=True, text=True).stdout)
+    return "\n".join(out)
+
+
+def kernel_body(txt, pat):
+    for f in re.split(r"\n(?=[0-9a-f]{16} <)", txt):
+        m = re.match(r"[0-9a-f]{16} <(\S+)>:", f)
+        if m and pat in m.group(1):
+            ins = []
+            for line in f.splitlines()[1:]:
+                mm = re.match(r"\s+([a-z_0-9]+)\s*(.*?)\s*//\s*([0-9A-F]+):", line)
+                if mm:
+                    ins.append((mm.group(1), mm.group(2), int(mm.group(3), 16)))
+            return m.group(1), ins
+    raise SystemExit(f"no kernel matching {pat!r}")
+
+
+def branch_target(ins, k):
+    """Index of the target of the branch at k (simm16 words after the next instruction)."""
+    op, args, addr = ins[k]
+    off = int(args.split()[0])
+    if off >= 32768:
+        off -= 65536
+    nxt = ins[k + 1][2] if k + 1 < len(ins) else addr + 4
+    tgt = nxt + 4 * off
+    for i, (_, _, a) in enumerate(ins):
+        if a == tgt:
+            return i
+    return None
+
+
+def main():
+    lib = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "sfmfromscratch_amd", "lib", "libsfmfeat.so")
+    pat = sys.argv[2] if len(sys.argv) > 2 else "k_harrisILi7ELb1ELi0ELi0E"
+    name, ins = kernel_body(disassemble(lib), pat)
+    # the tile loop: the backward branch with the largest span
+    loop = None
+    for k, (op, args, _) in enumerate(ins):
+        if op in ("s_branch", "s_cbranch_execz", "s_cbranch_execnz", "s_cbranch_scc0", "s_cbranch_scc1",
+                  "s_cbranch_vccz", "s_cbranch_vccnz"):
+            t = branch_target(ins, k)
+            if t is not None and t < k and (loop is None or k - t > loop[1] - loop[0]):
+                loop = (t, k)
+    a, b = loop
+    bars = [k for k in range(a, b + 1) if ins[k][0] == "s_barrier"]
+    # small backward loops inside the tile loop: the Sobel strip loops
+    inner = []
+    for k in range(a, b + 1):
+        op = ins[k][0]
+        if op.startswith("s_cbranch") or op == "s_branch":
+            t = branch_target(ins, k)
+            if t is not None and a < t < k and (k - t) < 400 and any(ins[i][0] == "v_pk_fma_f32" for i in range(t, k)):
+                inner.append((t, k))
+    NT, PH, NS = 256, 70, 18
+    trips = -(-PH * NS // NT)
+    cnt = collections.Counter()
+    hist_ops = {"v_not_b32_e32", "v_lshrrev_b32_e32", "v_and_b32_e32"}
+    for k in range(a, b + 1):
+        op = ins[k][0]
+        if not op.startswith("v_") and not op.startswith("ds_add"):
+            continue
+        in_inner = [(t, e) for t, e in inner if t <= k <= e]
+        if in_inner:
+            # the interior variant (the shorter loop) is the one interior tiles run
+            if in_inner[0] == min(inner, key=lambda te: te[1] - te[0]):
+                cnt["sobel (x%d strips)" % trips] += trips
+            continue
+        if op in ("v_pk_fma_f32", "v_fmac_f32_e32", "v_fma_f32"):
+            cnt["window fmas"] += 1
+        elif op == "v_pk_mul_f32":
+            cnt["products"] += 1
+        elif op in ("v_mul_f32_e32", "v_sub_f32_e32", "v_add_f32_e32"):
+            cnt["R (det - alpha tr^2)"] += 1
+        elif op in hist_ops or op.startswith("ds_add"):
+            cnt["histogram key + LDS add"] += 1
+        elif op.startswith(("v_cmp", "v_cndmask")):
+            cnt["masks (tile copy, hist bounds)"] += 1
+        else:
+            cnt["addressing / moves"] += 1
+    tot = sum(cnt.values())
+    print(f"{name}: tile loop {b - a + 1} instructions, {len(bars)} barriers, sobel loops {len(inner)} "
+          f"(trip count {trips})")
+    print(f"{'phase':22s} {'VALU/tile-wave':>14s} {'share':>7s}")
+    for k, v in sorted(cnt.items(), key=lambda kv: -kv[1]):
+        print(f"{k:22s} {v:14.0f} {v / tot:7.1%}")
+    print(f"{'total':22s} {tot:14.0f}")
+    win = sum(1 for k in range(a, b + 1) if ins[k][0] == "v_pk_fma_f32" and not any(t <= k <= e for t, e in inner))
+    sc = sum(1 for k in range(a, b + 1) if ins[k][0] in ("v_fmac_f32_e32", "v_fma_f32"))
+    print(f"window: {win} v_pk_fma_f32 + {sc} scalar fmas = {2 * win + sc} fmas "
+          f"(16 px x 147 = 2352 per tile-thread)")
+
+
+if __name__ == "__main__":
+    main()

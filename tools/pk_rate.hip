@@ -115,9 +115,12 @@ int main(int argc, char** argv) {
         maxocc = ++occ[key] > maxocc ? occ[key] : maxocc;
       }
       const double mean = sc / (4 * grid.x);
-      printf("%-26s waves/SIMD %d: %.3f ms, cycles per instruction per SIMD %.2f (max wave) %.2f (mean wave), %.0f MHz\n",
-             names[mode], maxocc, ms, mc / ((double)iters * 16 * maxocc), mean / ((double)iters * 16 * maxocc),
-             mc / (ms * 1e-3) / 1e6);
+      const double mhz = mc / (ms * 1e-3) / 1e6;  // s_memtime ticks over the launch
+      (void)maxocc;
+      (void)mean;
+      // one 256-thread workgroup = one wave per SIMD, so wps workgroups per CU = wps waves per SIMD
+      printf("%-26s waves/SIMD %d: %.3f ms at %.0f MHz -> %.2f cycles per wave instruction per SIMD\n", names[mode], wps,
+             ms, mhz, ms * 1e-3 * mhz * 1e6 / ((double)iters * 16 * wps));
       (void)hipEventDestroy(e0);
       (void)hipEventDestroy(e1);
     }
