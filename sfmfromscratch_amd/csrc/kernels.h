@@ -43,6 +43,10 @@ struct MedianState {
   uint32_t tnms;        // certified select: candidate threshold key
   uint32_t tcert;       // certified select: the k-th key must reach this
   uint32_t fallback;    // 1: this plane takes the exact path
+  // higher candidate thresholds (>= tnms): the buckets holding the 3 vmin / 8-th and
+  // vmin / 2-th largest values.  k_select first tries the candidates at or above them (a
+  // subset of about 2k-4k at vmin = 128 k, sorted whole), the full list when they are too few.
+  uint32_t tsub[2];
 };
 
 // Buckets from 2^126 up (and inf / NaN) never certify: (lo + hi) / 2 could overflow.
@@ -51,8 +55,8 @@ constexpr uint32_t kHugeBucket = 0x7F4u;
 // Per-plane select scan (median.hip k_med_scan; fused into the Harris kernel's last
 // workgroup of each plane): from the digit-1 histogram, the buckets holding the two
 // middle ranks (exact-median state) and the certified-select thresholds.  Needs 256 or
-// 512 threads (8 bins each for the first 256, one prefix pass for all three ranks); s_red
-// holds 8 u32.
+// 512 threads (8 bins each for the first 256, one prefix pass for all five ranks); s_red
+// holds 10 u32.
 // `hist` is read with agent-scope atomic loads so a fused caller sees every workgroup's
 // flush (L2 is per XCD); the 8 loads per thread are issued together.
 SFM_DEV void select_scan_plane(const uint32_t* hist, MedianState* st, unsigned long long* list_count,
@@ -82,9 +86,11 @@ SFM_DEV void select_scan_plane(const uint32_t* hist, MedianState* st, unsigned l
   const uint32_t k1 = (n % 2 == 1) ? (uint32_t)(n / 2) : (uint32_t)(n / 2 - 1);
   const uint32_t k2 = (uint32_t)(n / 2);
   const uint32_t kv = n > vmin ? (uint32_t)(n - vmin) : 0u;  // vmin-th largest value
-  const uint32_t ranks[3] = {k1, k2, kv};
+  const int64_t vs0 = 3 * vmin / 8, vs1 = vmin / 2;          // the subset thresholds' ranks
+  const uint32_t ks0 = n > vs0 ? (uint32_t)(n - vs0) : 0u, ks1 = n > vs1 ? (uint32_t)(n - vs1) : 0u;
+  const uint32_t ranks[5] = {k1, k2, kv, ks0, ks1};
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
+  for (int q = 0; q < 5; ++q) {
     const uint32_t r = ranks[q];
     if (r >= excl && r < excl + local) {  // exactly one thread owns each rank
       uint32_t c = excl;
@@ -106,6 +112,8 @@ SFM_DEV void select_scan_plane(const uint32_t* hist, MedianState* st, unsigned l
     const uint32_t tb = max(n > vmin ? s_red[4] : 0u, b1);
     const bool certifiable = !force_exact && b2 < kHugeBucket;
     st->tnms = tb << (32 - kMedBits1);
+    st->tsub[0] = max(n > vs0 ? s_red[6] : 0u, tb) << (32 - kMedBits1);
+    st->tsub[1] = max(n > vs1 ? s_red[8] : 0u, tb) << (32 - kMedBits1);
     st->tcert = certifiable ? (b2 + 1) << (32 - kMedBits1) : 0xffffffffu;
     st->fallback = certifiable ? 0u : 1u;
     st->bucket[0] = b1;

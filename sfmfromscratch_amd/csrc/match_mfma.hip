@@ -204,7 +204,10 @@ __device__ __forceinline__ void glds_x1(const void* gsrc, uint32_t lds_dst) {
 // The window argument: the targets achieving b1~ and b2~ have exact distances <= b1~ + E and
 // <= b2~ + E, so the exact second-smallest D2 <= b2~ + E; a target with exact d <= D2 has
 // d~ <= d + E <= b2~ + 2E.  Targets outside the window are strictly farther than D2.
-template <int STAGE>
+// ABL (diagnostic build only, SFMFEAT_MATCH_ABL; results wrong by design): 1 no epilogue
+// (MFMAs, fragment reads, stages and barriers only), 2 no MFMAs (the epilogue on unchanged
+// accumulators), 4 no admission masks / appends
+template <int STAGE, int ABL = 0>
 __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
     const int32_t* __restrict__ count, int64_t capP, const _Float16* __restrict__ hi,
     const _Float16* __restrict__ lo, const float* __restrict__ norm2, const float* __restrict__ rnorm,
@@ -355,6 +358,7 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   // 32 targets x 32 queries of sub-tile `sub` of the stage at byte offset `bofs`: hi.hi into
   // ahh, hi.lo + lo.hi into ax (one accumulation chain each)
   auto mfma_sub = [&](const int (&vb)[8], int sub, f32x16& ahh, f32x16& ax) {
+    if constexpr ((ABL & 2) != 0) return;
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       const h8 thi = *reinterpret_cast<const h8*>(smem + vb[kk] + sub * 32 * ROWB);
@@ -385,6 +389,10 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   // (b1, b2) the same way.  The admission mask is built only when some lane's smallest d~
   // passes the threshold (after the first stages, most sub-tiles admit nothing).
   auto epi = [&](const f32x16& ahh, const f32x16& ax, const float (&nb)[16], float (&d)[16], uint32_t& mm) {
+    if constexpr ((ABL & 1) != 0) {
+      asm volatile("" ::"v"(ahh), "v"(ax));  // keep the MFMAs
+      return;
+    }
 #pragma unroll
     for (int rr = 0; rr < 16; ++rr)
       d[rr] = __builtin_fmaf(ax[rr], -1.4901161193847656e-08f /* -2^-26 */,
@@ -409,7 +417,7 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
     // the row's b2~ so far over both halves (every lane's b2 and b1 >= its half's final ones)
     const float ob1 = other_half(b1), ob2 = other_half(b2);
     const float t = fminf(fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + E2, thr_w);
-    if (__any(tm <= t)) {
+    if ((ABL & 4) == 0 && __any(tm <= t)) {
 #pragma unroll
       for (int rr = 0; rr < 16; ++rr) mm |= (d[rr] <= t) ? (1u << rr) : 0u;
     }
@@ -949,14 +957,29 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
   const int qb = (max_rows + kQB - 1) / kQB;
   const dim3 grid((unsigned)(8 * ((P + 7) / 8) * qb));
   // ovf_count is zero here: set once at allocation, re-zeroed by k_match_compact
-#define SFM_SWEEP(A)                                                                                  \
-  hipLaunchKernelGGL(k_match_mfma<A>, grid, dim3(kNT), 0, st, count, capP, hi, lo, norm2, rnorm,        \
+#define SFM_SWEEP(A, ABL)                                                                             \
+  hipLaunchKernelGGL((k_match_mfma<A, ABL>), grid, dim3(kNT), 0, st, count, capP, hi, lo, norm2, rnorm,   \
                      static_cast<const float2*>(pmax), pairs, P, max_rows, cand, cand_n, cand_thr, ovf_count, \
                      ovf_list)
+  static const int abl = [] {  // timing ablations: diagnostic build only (SFM_ABLATION_ENV)
+    const char* e = SFM_ABLATION_ENV("SFMFEAT_MATCH_ABL");
+    return e ? atoi(e) : 0;
+  }();
+#ifdef SFM_ABLATIONS
+  switch (abl) {
+    case 1: SFM_SWEEP(1, 1); break;
+    case 2: SFM_SWEEP(1, 2); break;
+    case 4: SFM_SWEEP(1, 4); break;
+    case 6: SFM_SWEEP(1, 6); break;
+    default: if (stage == 0) SFM_SWEEP(0, 0); else SFM_SWEEP(1, 0);
+  }
+#else
+  (void)abl;
   if (stage == 0)
-    SFM_SWEEP(0);
+    SFM_SWEEP(0, 0);
   else
-    SFM_SWEEP(1);
+    SFM_SWEEP(1, 0);
+#endif
 #undef SFM_SWEEP
   // two (pair, row) items per wavefront above the eight-item kernel's range (round 4: match
   // stage 0.229 -> 0.223 ms/step at configs[1]); SFMFEAT_RERANK2=0: one item per wavefront (A/B)

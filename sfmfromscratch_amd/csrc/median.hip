@@ -19,7 +19,7 @@ __global__ void __launch_bounds__(256) k_med_scan(const uint32_t* __restrict__ h
                                                   MedianState* __restrict__ st,
                                                   unsigned long long* __restrict__ list_count,
                                                   int64_t n, int64_t vmin, int force_exact) {
-  __shared__ uint32_t s_red[8];
+  __shared__ uint32_t s_red[10];
   const int b = blockIdx.x;
   select_scan_plane(hist + (int64_t)b * kMedBins1, st + b, list_count + (int64_t)b * kCounterStride, n, vmin,
                     force_exact, s_red);

@@ -128,7 +128,8 @@ struct SelectLds {
 // scratch for tie lists that overflow LDS).
 // abl (timing ablations, results wrong by design; SFMFEAT_SELECT_ABL): 1 no final sort, 2 no
 // radix select (every key counts as below the k-th); k_select: 4 no exact median, 8 no exact NMS;
-// 16 (a correct variant, A/B): wave-aggregated histogram adds (hist_add)
+// 16 (a correct variant, A/B): wave-aggregated histogram adds (hist_add); 32 (correct, A/B,
+// SFMFEAT_SELECT_SUBSET=0): no subset fast path (topk_subset)
 SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, const SelectLds& L, int abl = 0) {
   const int tid = threadIdx.x, nt = blockDim.x;
   if (C <= kTopkDirect) {
@@ -206,6 +207,71 @@ SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, co
   sort_keys_u64(L.sel, kk);
 }
 
+// Wave-aggregated append to an LDS counter: the lane's slot, or -1 without pred.
+SFM_DEV int lds_wave_append(uint32_t* counter, bool pred) {
+  const uint64_t mask = __ballot(pred);
+  if (mask == 0) return -1;
+  const int lane = __lane_id();
+  const int leader = __ffsll((unsigned long long)mask) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+  base = __shfl(base, leader);
+  const uint64_t lower = mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane)));
+  return pred ? (int)(base + (uint32_t)__popcll(lower)) : -1;
+}
+
+// Certified planes with more than kTopkDirect candidates: the candidates at or above a higher
+// threshold tsub[t] (MedianState) — the 3 vmin / 8-th or vmin / 2-th largest value's bucket,
+// about 1-3k keys at vmin = 128 k instead of 3-7k — when at least kk (and at most kTopkDirect)
+// of them exist.  Every candidate outside that subset lies below its threshold, i.e. below
+// each of its members, so its kk best keys are the whole list's kk best (the caller's
+// certification test then applies unchanged).  Sorted whole in L.sel; true when taken, false
+// (nothing written) when neither subset fits: the caller runs the full top-k.
+SFM_DEV bool topk_subset(const uint64_t* cp, int64_t C, int kk, const uint32_t (&tsub)[2], uint32_t tnms,
+                         const SelectLds& L) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (C <= kTopkDirect || C > (int64_t)kRegKeys * nt || tsub[1] <= tnms) return false;
+  uint64_t kr[kRegKeys];
+#pragma unroll
+  for (int j = 0; j < kRegKeys; ++j) {
+    const int64_t i = tid + (int64_t)nt * j;
+    kr[j] = i < C ? cp[i] : ~0ull;  // ~0: high half 0xffffffff, below every threshold
+  }
+  // candidate keys hold ~fkey(R) in their high half: fkey(R) >= t  <=>  hi <= ~t
+  const uint32_t h0 = ~tsub[0], h1 = ~tsub[1];
+  if (tid < 2) L.cnt[tid] = 0u;
+  __syncthreads();
+  uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+  for (int j = 0; j < kRegKeys; ++j) {
+    const uint32_t hi = (uint32_t)(kr[j] >> 32);
+    c0 += (uint32_t)__popcll(__ballot(hi <= h0));
+    c1 += (uint32_t)__popcll(__ballot(hi <= h1));
+  }
+  if ((tid & 63) == 0) {
+    atomicAdd(&L.cnt[0], c0);
+    atomicAdd(&L.cnt[1], c1);
+  }
+  __syncthreads();
+  const uint32_t n0 = L.cnt[0], n1 = L.cnt[1];
+  const int t = (n0 >= (uint32_t)kk && n0 <= (uint32_t)kTopkDirect) ? 0
+              : (n1 >= (uint32_t)kk && n1 <= (uint32_t)kTopkDirect) ? 1 : -1;
+  if (t < 0) return false;  // (uniform)
+  const uint32_t ht = t == 0 ? h0 : h1;
+  __syncthreads();
+  if (tid == 0) L.cnt[0] = 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kRegKeys; ++j) {
+    const bool in = (uint32_t)(kr[j] >> 32) <= ht;
+    const int slot = lds_wave_append(&L.cnt[0], in);
+    if (in) L.sel[slot] = kr[j];
+  }
+  __syncthreads();
+  sort_keys_u64(L.sel, (int)(t == 0 ? n0 : n1));
+  return true;
+}
+
 // Edge filter with order-preserving compaction of L.sel[0..nsel) into the plane's list.
 SFM_DEV void emit_keypoints(const SelectLds& L, int nsel, KpList kp, int b, int kcap, int H, int W, int hw) {
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -232,19 +298,6 @@ SFM_DEV void emit_keypoints(const SelectLds& L, int nsel, KpList kp, int b, int 
     }
   }
   if (tid == 0) kp.count[b] = (int32_t)total;
-}
-
-// Wave-aggregated append to an LDS counter: the lane's slot, or -1 without pred.
-SFM_DEV int lds_wave_append(uint32_t* counter, bool pred) {
-  const uint64_t mask = __ballot(pred);
-  if (mask == 0) return -1;
-  const int lane = __lane_id();
-  const int leader = __ffsll((unsigned long long)mask) - 1;
-  uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
-  base = __shfl(base, leader);
-  const uint64_t lower = mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane)));
-  return pred ? (int)(base + (uint32_t)__popcll(lower)) : -1;
 }
 
 // Both middle keys from the collected list at once: digit 2 (11 bits) of rank r1 in bucket b1
@@ -521,7 +574,9 @@ __global__ void __launch_bounds__(1024) k_select(SelectLevels g, int kcap, int k
   if (!s.fallback) {
     const int64_t C = (int64_t)cand_count[(int64_t)b * kCounterStride];  // certified NMS's candidates
     if (C >= (int64_t)k) {
-      topk_sorted(cp, C, k, tp, L, abl);
+      // SFMFEAT_SELECT_SUBSET=0 (A/B): always the full candidate list
+      if (!(abl & 32) && !topk_subset(cp, C, k, s.tsub, s.tnms, L)) topk_sorted(cp, C, k, tp, L, abl);
+      else if (abl & 32) topk_sorted(cp, C, k, tp, L, abl);
       if ((abl & 3) || ~(uint32_t)(L.sel[k - 1] >> 32) >= s.tcert) {  // k-th candidate above the median's bucket
         emit_keypoints(L, k, kp, b, kcap, H, W, hw);
         return;
@@ -552,7 +607,8 @@ void launch_select_levels(const SelectLevels& g, int kcap, int k, int B, int ksi
   if (g.n < 1 || g.n > kSelectMaxLevels || B < 1) return;
   static const int abl = [] {
     const char* e = SFM_ABLATION_ENV("SFMFEAT_SELECT_ABL");
-    return e ? atoi(e) : 0;
+    const char* sb = getenv("SFMFEAT_SELECT_SUBSET");  // a correct variant (A/B): 0 = full list always
+    return (e ? atoi(e) : 0) | ((sb && atoi(sb) == 0) ? 32 : 0);
   }();
   hipLaunchKernelGGL(k_select, dim3(B * g.n), dim3(1024), topk_lds_bytes(), st, g, kcap, k, ksize / 2, B, abl);
 }

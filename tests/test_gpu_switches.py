@@ -5,6 +5,7 @@ process (same GPU, same inputs) and this process holds the defaults:
   SFMFEAT_PYR_FUSED=0   pyramid levels 1-3 by k_down2x3 instead of the level-0 k_harris launch
   SFMFEAT_RERANK2=0     one query row per wavefront in the matcher's exact re-rank
   SFMFEAT_EXACT_PX=64   4K level 3 tries certification before its exact path
+  SFMFEAT_SELECT_SUBSET=0  certified top-k always from the full candidate list (no subset fast path)
 Cases: 4 x 1080p at P-oct (four exact 2x levels: the fused pyramid) and 2 x 4K at five
 levels, k = 8000 (fused levels 1-3 plus a trailing k_down2, exact level 3).
 """
@@ -25,7 +26,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = {"1080p": (4, 1080, 1920, dict(P_OCT, num_interest_points=2500)),
          "4k": (2, 2160, 3840, dict(P_OCT, num_interest_points=8000, pyramid_level=5))}
-ALT_ENV = {"SFMFEAT_PYR_FUSED": "0", "SFMFEAT_RERANK2": "0", "SFMFEAT_EXACT_PX": "64"}
+ALT_ENV = {"SFMFEAT_PYR_FUSED": "0", "SFMFEAT_RERANK2": "0", "SFMFEAT_EXACT_PX": "64", "SFMFEAT_SELECT_SUBSET": "0"}
 
 
 def run_cases() -> dict:
