@@ -96,7 +96,7 @@ __device__ int64_t g_harris_stamps_cap;  // u64 slots behind g_harris_stamps (wo
 
 // NPAIR: output row pairs per thread.  2: 256 threads x (4 columns x 4 rows), 2 waves per
 // SIMD at up to 256 VGPRs.  1: 512 threads x (4 columns x 2 rows), 4 waves per SIMD at up to
-// 128 VGPRs (the window's packed fmas issue faster at 4 waves per SIMD), at
+// 128 VGPRs (the window's packed fmas issue faster at 4 waves per SIMD, DESIGN_LOG.md §B), at
 // the price of each gradient row's products being formed by twice as many threads.
 // F (the workgroup form):
 //   0: 256 threads x (4 columns x 4 rows), 64 x 64 tiles, 2 workgroups per CU (2 waves per
@@ -209,7 +209,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   // tap pairs per gradient row r and row pair p: (g[r-2p][j], g[r-2p-1][j]), 0 where the
   // tap row does not exist; read as uniform LDS broadcasts (49 taps in SGPRs spill)
   __shared__ __attribute__((aligned(16))) f32x2 s_tp[KS + 2 * NPAIR - 1][NPAIR][KS + (KS & 1)];
-  __shared__ uint32_t s_last, s_red[8];
+  __shared__ uint32_t s_last, s_red[10];
 
   const int tid = threadIdx.x;
   const int b = blockIdx.y;
@@ -300,17 +300,27 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     const int tx0 = (tile % tiles_x) * kHT;
     const int ty0 = (tile / tiles_x) * TH;
     __syncthreads();  // the previous tile's LDS reads are done
-    // 0. the prefetched image tile -> LDS, then start fetching the next tile
+    // 0. the prefetched image tile -> LDS, then start fetching the next tile (a tile whose
+    //    whole image window lies inside the image stores its loads unmasked)
+    const bool img_in = tx0 - XA >= 0 && tx0 - XA + IWP <= W && ty0 - GA - 1 >= 0 && ty0 - GA - 1 + IH <= H;
+    if (VEC && img_in) {
 #pragma unroll
-    for (int k = 0; k < NIMG; ++k) {
-      const bool ok = (okmask >> k) & 1ull;
-      if constexpr (VEC) {
+      for (int k = 0; k < NIMG; ++k) {
         const int e = tid + NT * k;
-        if (e < IH * IW4)
-          reinterpret_cast<f32x4*>(&s_img[0][0])[e] = ok ? t4[k] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      } else {
-        const int e = tid + NT * k;
-        if (e < IH * IWP) (&s_img[0][0])[e] = ok ? t1[k] : 0.0f;
+        if (e < IH * IW4) reinterpret_cast<f32x4*>(&s_img[0][0])[e] = t4[VEC ? k : 0];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < NIMG; ++k) {
+        const bool ok = (okmask >> k) & 1ull;
+        if constexpr (VEC) {
+          const int e = tid + NT * k;
+          if (e < IH * IW4)
+            reinterpret_cast<f32x4*>(&s_img[0][0])[e] = ok ? t4[k] : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        } else {
+          const int e = tid + NT * k;
+          if (e < IH * IWP) (&s_img[0][0])[e] = ok ? t1[k] : 0.0f;
+        }
       }
     }
     __syncthreads();
@@ -638,36 +648,43 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
       }
     });
     // 3. R = det - alpha * trace^2 (:71-74), digit-1 histogram of R, R stored as 16-B
-    //    row segments (a wave writes 8 rows x 128 contiguous bytes per store)
+    //    row segments (a wave writes 8 rows x 128 contiguous bytes per store); a tile wholly
+    //    inside the plane counts and stores without per-pixel bounds
+    auto epilogue = [&](auto fullc) {
+      constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
-    for (int o = 0; o < RPT; ++o) {
-      const int gy = ty0 + RPT * rq + o;
-      const int gx0 = tx0 + 4 * tq;
-      float Rq[4];
+      for (int o = 0; o < RPT; ++o) {
+        const int gy = ty0 + RPT * rq + o;
+        const int gx0 = tx0 + 4 * tq;
+        float Rq[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float sxx = acc[o >> 1][0][q][o & 1], syy = acc[o >> 1][1][q][o & 1],
-                    sxy = HY ? macc2[HY ? o : 0][q] : acc[o >> 1][2][q][o & 1];
-        const float t1v = sxx * syy;
-        const float t2v = sxy * sxy;
-        const float det = t1v - t2v;
-        const float tr = sxx + syy;
-        const float tr2 = tr * tr;
-        const float at = alpha * tr2;
-        Rq[q] = det - at;
-        if (ABL != 1) atomicAdd(&s_hist[fkey(Rq[q]) >> (32 - kMedBits1)], (gy < H && gx0 + q < W) ? 1u : 0u);
-      }
-      if (gy < H) {
-        float* dst = Rp + (int64_t)gy * W + gx0;
-        if (VEC) {
-          if (gx0 < W) *reinterpret_cast<float4*>(dst) = make_float4(Rq[0], Rq[1], Rq[2], Rq[3]);
-        } else {
+        for (int q = 0; q < 4; ++q) {
+          const float sxx = acc[o >> 1][0][q][o & 1], syy = acc[o >> 1][1][q][o & 1],
+                      sxy = HY ? macc2[HY ? o : 0][q] : acc[o >> 1][2][q][o & 1];
+          const float t1v = sxx * syy;
+          const float t2v = sxy * sxy;
+          const float det = t1v - t2v;
+          const float tr = sxx + syy;
+          const float tr2 = tr * tr;
+          const float at = alpha * tr2;
+          Rq[q] = det - at;
+          if (ABL != 1)
+            atomicAdd(&s_hist[fkey(Rq[q]) >> (32 - kMedBits1)], (FULL || (gy < H && gx0 + q < W)) ? 1u : 0u);
+        }
+        if (FULL || gy < H) {
+          float* dst = Rp + (int64_t)gy * W + gx0;
+          if (VEC) {
+            if (FULL || gx0 < W) *reinterpret_cast<float4*>(dst) = make_float4(Rq[0], Rq[1], Rq[2], Rq[3]);
+          } else {
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (gx0 + q < W) dst[q] = Rq[q];
+            for (int q = 0; q < 4; ++q)
+              if (FULL || gx0 + q < W) dst[q] = Rq[q];
+          }
         }
       }
-    }
+    };
+    if (ty0 + TH <= H && tx0 + kHT <= W) epilogue(std::true_type{});
+    else epilogue(std::false_type{});
     }  // !MF
     if constexpr (ABL == 3) {
       if (tid == 0 && stamp && nst < kStampSlots - 4) stamp[4 + nst] = wall_clock64();
@@ -731,7 +748,7 @@ static void launch_form(HarrisLevels g, int B, const float* gk, float alpha, hip
   // of >= 16 planes take 448 = 14 workgroups per plane at 32 planes, which leaves 64 CUs
   // with one Harris workgroup instead of two for the other batch in flight: measured 33.4k
   // -> 34.8-35.5k img/s on the headline (13 per plane: 33.0k, 15: 32.5k, 16: 33.4k, 18:
-  // 34.2-34.6k); at 8 planes of 4K 448 cost 6 % and 480 (60 per plane)
+  // 34.2-34.6k; DESIGN_LOG.md §B); at 8 planes of 4K 448 cost 6 % and 480 (60 per plane)
   // measured best (6.15-6.17k against 5.98-6.00k img/s at 512, 5.95k at 576, 5.87k at 640).
   static const int slots_env = env_int("SFMFEAT_HARRIS_SLOTS", 0);
   // SFMFEAT_HARRIS_SLOTS_UPPER=n (A/B): the budget of levels above the first (fewer than

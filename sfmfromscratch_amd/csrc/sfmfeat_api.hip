@@ -426,7 +426,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   };
   // Harris launches: one per level, unless SFMFEAT_HARRIS_GROUP=g (g >= 1): levels >= g then
   // share launches (up to kHarrisMaxLevels each).  Off by default: grouping L1-L3 or L2-L3 cut
-  // the Harris stage time by ~2% but the pipeline lost more overlap than that.
+  // the Harris stage time by ~2% but the pipeline lost more overlap than that (DESIGN_LOG.md §B).
   static const int group_from = [] {
     const char* e = getenv("SFMFEAT_HARRIS_GROUP");
     return e ? atoi(e) : 0;
