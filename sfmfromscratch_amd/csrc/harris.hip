@@ -87,7 +87,8 @@ __device__ __forceinline__ void pk_fma_bcast(f32x2& acc, f32x2 k, f32x2 v) {
 // registers one tile ahead.
 //
 // ABL (timing builds only): 0 = full kernel, 1 = no digit histogram, 2 = window sums over
-// the first tap row only, 3 = full kernel + per-workgroup timestamps into g_harris_stamps.
+// the first tap row only, 3 = full kernel + per-workgroup timestamps into g_harris_stamps,
+// 4 = no workgroup barriers in the tile loop (LDS races: results wrong; the barriers' cost).
 // ABL = 3 diagnostics: per workgroup kStampSlots u64 = {start, end, cu id, tiles, end of
 // each tile ...} (s_memrealtime, 100 MHz)
 constexpr int kStampSlots = 48;
@@ -299,7 +300,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     }
     const int tx0 = (tile % tiles_x) * kHT;
     const int ty0 = (tile / tiles_x) * TH;
-    __syncthreads();  // the previous tile's LDS reads are done
+    if constexpr (ABL != 4) __syncthreads();  // the previous tile's LDS reads are done
     // 0. the prefetched image tile -> LDS, then start fetching the next tile (a tile whose
     //    whole image window lies inside the image stores its loads unmasked)
     const bool img_in = tx0 - XA >= 0 && tx0 - XA + IWP <= W && ty0 - GA - 1 >= 0 && ty0 - GA - 1 + IH <= H;
@@ -323,7 +324,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
         }
       }
     }
-    __syncthreads();
+    if constexpr (ABL != 4) __syncthreads();
     // (PP: after the product pass, so the prefetch registers are not live beside the
     // strips' gradients)
     if (!PP && tile + nwg < ntiles) prefetch(tile + nwg);
@@ -427,7 +428,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     const bool grad_in = tx0 - GA >= 0 && tx0 - GA + PWP <= W && ty0 - GA >= 0 && ty0 - GA + PH <= H;
     if (grad_in) sobel(std::false_type{});
     else sobel(std::true_type{});
-    __syncthreads();
+    if constexpr (ABL != 4) __syncthreads();
     if constexpr (F == 0) {
       // fused pyramid: the tile's 8 x 8 blocks of this level -> the next three exact 2x levels
       // (pyramid.hip k_down2x3's arithmetic, so the levels are bit-identical), one block per
@@ -873,6 +874,7 @@ float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, 
       case 1: launch_ks<7, 1>(g, B, gk, alpha, 0); break;
       case 2: launch_ks<7, 2>(g, B, gk, alpha, 0); break;
       case 3: launch_ks<7, 3>(g, B, gk, alpha, 0); break;
+      case 4: launch_ks<7, 4>(g, B, gk, alpha, 0); break;
       default: launch_ks<7, 0>(g, B, gk, alpha, 0); break;
     }
   };

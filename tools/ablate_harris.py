@@ -7,5 +7,5 @@ f = L.sfm_debug_time_harris
 f.restype = ctypes.c_float
 f.argtypes = [ctypes.c_int32] * 6
 for B, H, W in [(32, 1080, 1920)]:
-    for abl, name in [(0, "full"), (1, "no-hist"), (2, "window-1row"), (0, "full")]:
+    for abl, name in [(0, "full"), (1, "no-hist"), (2, "window-1row"), (4, "no-barriers"), (0, "full")]:
         print(f"B={B} {H}x{W} {name:10s} {f(0, abl, B, H, W, 20):8.3f} ms", flush=True)
