@@ -206,7 +206,14 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   __shared__ __attribute__((aligned(16))) float s_pl[NPL * PH * PWP + (PP ? 0 : IH * IWP)];
   float (*const s_g)[PH][PWP] = reinterpret_cast<float (*)[PH][PWP]>(s_pl);
   float (*const s_img)[IWP] = reinterpret_cast<float (*)[IWP]>(s_pl + (PP ? 0 : NPL * PH * PWP));
-  __shared__ uint32_t s_hist[kMedBins1];  // digit-1 histogram, flushed once per workgroup
+  // digit-1 histogram, flushed once per workgroup: two copies (even / odd lanes, the second
+  // shifted by half the banks) where the LDS budget of WPC workgroups per CU allows, halving
+  // the same-address serialisation of one wave's LDS adds
+  constexpr int kHistCopy = kMedBins1 + 32;
+  constexpr int kLdsRest = 4 * (NPL * PH * PWP + (PP ? 0 : IH * IWP)) +
+                           8 * (KS + 2 * NPAIR - 1) * NPAIR * (KS + (KS & 1)) + 1024;
+  constexpr int NHC = kLdsRest + 8 * kHistCopy <= 163840 / HarrisShape<F>::WPC ? 2 : 1;
+  __shared__ uint32_t s_hist[NHC * kHistCopy];
   // tap pairs per gradient row r and row pair p: (g[r-2p][j], g[r-2p-1][j]), 0 where the
   // tap row does not exist; read as uniform LDS broadcasts (49 taps in SGPRs spill)
   __shared__ __attribute__((aligned(16))) f32x2 s_tp[KS + 2 * NPAIR - 1][NPAIR][KS + (KS & 1)];
@@ -226,13 +233,14 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   }
   const float* img = lvl + (int64_t)b * H * W;
   float* Rp = Rout + (int64_t)b * H * W;
-  for (int i = tid; i < kMedBins1; i += NT) s_hist[i] = 0u;
+  for (int i = tid; i < NHC * kHistCopy; i += NT) s_hist[i] = 0u;
   for (int i = tid; i < (KS + 2 * NPAIR - 1) * NPAIR * KS; i += NT) {
     const int r = i / (NPAIR * KS), p = (i / KS) % NPAIR, j = i % KS;
     const int i0 = r - 2 * p, i1 = i0 - 1;
     s_tp[r][p][j] = f32x2{(i0 >= 0 && i0 < KS) ? gk[i0 * KS + j] : 0.0f, (i1 >= 0 && i1 < KS) ? gk[i1 * KS + j] : 0.0f};
   }
   const int lane = tid & 63, wv = tid >> 6;
+  uint32_t* const s_hc = s_hist + (NHC == 2 ? (lane & 1) * kHistCopy : 0);
   // MFMA window: the banded tap operand A(dy, s), lane 4b+i: g[dy][s - i] (0 off the band).
   // Every block of an A operand holds the same taps, so the instruction's A broadcast
   // (cbsz 4: block abid's A to all 16 blocks; tools/mfma_f32_probe.hip) lets one VGPR carry
@@ -538,7 +546,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
           const float tr2 = tr * tr;
           const float at = alpha * tr2;
           Rq[i] = det - at;
-          if (ABL != 1) atomicAdd(&s_hist[fkey(Rq[i]) >> (32 - kMedBits1)], (gy < H && gx0 + i < W) ? 1u : 0u);
+          if (ABL != 1) atomicAdd(&s_hc[fkey(Rq[i]) >> (32 - kMedBits1)], (gy < H && gx0 + i < W) ? 1u : 0u);
         }
         if (gy < H) {
           float* dst = Rp + (int64_t)gy * W + gx0;
@@ -670,7 +678,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
           const float at = alpha * tr2;
           Rq[q] = det - at;
           if (ABL != 1)
-            atomicAdd(&s_hist[fkey(Rq[q]) >> (32 - kMedBits1)], (FULL || (gy < H && gx0 + q < W)) ? 1u : 0u);
+            atomicAdd(&s_hc[fkey(Rq[q]) >> (32 - kMedBits1)], (FULL || (gy < H && gx0 + q < W)) ? 1u : 0u);
         }
         if (FULL || gy < H) {
           float* dst = Rp + (int64_t)gy * W + gx0;
@@ -701,7 +709,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   __syncthreads();
   uint32_t* hg = hist_g + (int64_t)b * kMedBins1;
   for (int i = tid; i < kMedBins1; i += NT) {
-    uint32_t c = s_hist[i];
+    uint32_t c = s_hist[i] + (NHC == 2 ? s_hist[kHistCopy + i] : 0u);
     if (c) atomicAdd(&hg[i], c);
   }
   if (scan.state == nullptr) return;

@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   static_assert((size_t)OFF_D + kDBytes <= kSweepLds, "LDS carve");
   __shared__ __attribute__((aligned(16))) unsigned char smem[kSweepLds];
   float* const sNb = reinterpret_cast<float*>(smem + OFF_N);  // [NNB][kTT2]
-  float* const sDb = reinterpret_cast<float*>(smem + OFF_D);  // [kWaves][64][16]
+  float* const sDb = reinterpret_cast<float*>(smem + OFF_D);  // [kWaves][8][64] float2
 
   // XCD-aware mapping (workgroups b and b + 8 share an XCD and its L2): group g = b % 8
   // takes the pairs p = g (mod 8), so all query blocks of a pair stream its target table
@@ -444,19 +444,22 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   auto pin = [](float x1, float x2, uint32_t mm) { asm volatile("" ::"v"(x1), "v"(x2), "v"(mm)); };
   // admitted elements of one sub-tile (bit rr of mm, targets jb + 8 (rr >> 2) + 4 half +
   // (rr & 3)) -> the row's global list as (index | d~ rounded down to bf16 << 16).  When
-  // any lane of the wave admits, the lane's 16 d~ go to its LDS row (4 x 16-B stores) and
-  // each admitted one is read back by index (no dynamic register indexing into d)
-  float* my_d = sDb + (wid * 64 + lane) * 16;
+  // any lane of the wave admits, the lane's 16 d~ go to the wave's LDS area (no dynamic
+  // register indexing into d) and each admitted one is read back by index.  Layout
+  // [pair rr / 2][lane] of float2: the 8-B stores cover all 32 banks per 16-lane group and a
+  // read of element rr hits bank 2 lane + (rr & 1) (mod 32), so lanes reading different rr
+  // conflict at most 2-way (a lane-major [lane][16] row put 4 lanes on the same banks)
+  float2* const my_d2 = reinterpret_cast<float2*>(sDb) + wid * 8 * 64 + lane;
   auto append = [&](uint32_t mm, const float (&d)[16], int jb) {
     if (__any(mm != 0u)) {  // wave-uniform: skip when no lane admits
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        *reinterpret_cast<float4*>(my_d + 4 * q) = make_float4(d[4 * q], d[4 * q + 1], d[4 * q + 2], d[4 * q + 3]);
+      for (int q = 0; q < 8; ++q) my_d2[64 * q] = make_float2(d[2 * q], d[2 * q + 1]);
       if (live && mm) {
         for (; mm; mm &= mm - 1, ++cnt) {
           const int rr = __builtin_ctz(mm);
+          const float dr = reinterpret_cast<const float*>(my_d2 + 64 * (rr >> 1))[rr & 1];
           if (cnt < kHalfCap)
-            my_list[cnt] = (uint32_t)(jb + 4 * half + (rr & 3) + 8 * (rr >> 2)) | ((uint32_t)bf16_down(my_d[rr]) << 16);
+            my_list[cnt] = (uint32_t)(jb + 4 * half + (rr & 3) + 8 * (rr >> 2)) | ((uint32_t)bf16_down(dr) << 16);
         }
       }
     }
@@ -969,6 +972,7 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
   switch (abl) {
     case 1: SFM_SWEEP(1, 1); break;
     case 2: SFM_SWEEP(1, 2); break;
+    case 3: SFM_SWEEP(1, 3); break;
     case 4: SFM_SWEEP(1, 4); break;
     case 6: SFM_SWEEP(1, 6); break;
     default: if (stage == 0) SFM_SWEEP(0, 0); else SFM_SWEEP(1, 0);
