@@ -324,6 +324,13 @@ float sfm_debug_time_harris(int32_t device, int32_t abl, int32_t B, int32_t H, i
 float sfm_debug_harris_stamps(int32_t device, int32_t abl, int32_t B, int32_t H, int32_t W,
                               int32_t iters, uint64_t* out, int64_t cap);
 
+/* Diagnostic build only (make ABLATIONS=1; -1 in the shipped library): the matcher sweep's
+ * per-wave shader-clock stamps of its last launch under SFMFEAT_MATCH_ABL=32, u64
+ * [16 workgroups][8 waves][41][4] (stages 0..39: after the stage barrier, after each sub-tile
+ * region, after the DMA issue; row 40: start clock, start / end realtime, pair | stages << 32),
+ * then u64 [1024 workgroups][4]: start / end realtime, __smid(), pair | row0 << 32. */
+int64_t sfm_debug_match_stamps(uint64_t* out, int64_t cap);
+
 /* Keypoint selection of the context's last extraction (synchronises the device): planes
  * (image x level) that took the exact-median path, and planes in total.  The default
  * certified select decides the others from the Harris histogram alone. */

@@ -73,6 +73,7 @@ SIGNATURES = {
     "sfm_profile_read": (ctypes.c_int32, [_vp, ctypes.POINTER(ctypes.c_double), _i64p, ctypes.c_int32]),
     "sfm_debug_time_harris": (ctypes.c_float, [ctypes.c_int32] * 6),
     "sfm_debug_harris_stamps": (ctypes.c_float, [ctypes.c_int32] * 6 + [ctypes.c_void_p, ctypes.c_int64]),
+    "sfm_debug_match_stamps": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int64]),
     "sfm_debug_select_stats": (ctypes.c_int32, [_vp, _i32p, _i32p]),
 
     "sfm_debug_copy_level": (ctypes.c_int32, [_vp, ctypes.c_int32, ctypes.c_int32, _vp, _vp]),

@@ -169,4 +169,7 @@ float sfm_debug_harris_stamps(int32_t device, int32_t abl, int32_t B, int32_t H,
   return ms;
 }
 
+// The matcher sweep's per-wave clock stamps (diagnostic build, SFMFEAT_MATCH_ABL=32).
+int64_t sfm_debug_match_stamps(uint64_t* out, int64_t cap) { return sfm::match_stamps_copy(out, cap); }
+
 }  // extern "C"

@@ -227,6 +227,9 @@ struct HarrisLevels {
 void launch_harris_levels(const HarrisLevels& g, int B, const float* d_gauss, int ks, float alpha,
                           hipStream_t st);
 
+int64_t match_stamps_copy(uint64_t* out, int64_t cap);
+// words of the sweep's work-unit list (k_match_units) for P pairs of up to max_rows rows
+size_t match_units_words(int P, int max_rows);
 float time_harris_ablation(int abl, const float* lvl, float* R, uint32_t* hist, int B, int H, int W,
                            const float* gk, float alpha, int iters, uint64_t* stamps = nullptr,
                            int64_t stamps_cap = 0);
@@ -316,6 +319,6 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
                        const _Float16* hi, const _Float16* lo, const float* norm2, const float* rnorm,
                        const void* pmax, const int32_t* pairs, int P, float ratio,
                        RowBest* rows, int max_rows, uint32_t* cand, int32_t* cand_n, float* cand_thr,
-                       int* ovf_count, int2* ovf_list, hipStream_t st);
+                       int* ovf_count, int2* ovf_list, int32_t* units, hipStream_t st);
 
 }  // namespace sfm

@@ -206,14 +206,61 @@ __device__ __forceinline__ void glds_x1(const void* gsrc, uint32_t lds_dst) {
 // d~ <= d + E <= b2~ + 2E.  Targets outside the window are strictly farther than D2.
 // ABL (diagnostic build only, SFMFEAT_MATCH_ABL; results wrong by design): 1 no epilogue
 // (MFMAs, fragment reads, stages and barriers only), 2 no MFMAs (the epilogue on unchanged
-// accumulators), 4 no admission masks / appends
+// accumulators), 4 no admission masks / appends, 16 fragment reads of k-step 0 only (reused
+// for all eight: no LDS latency inside a sub-tile), 32 full sweep + clock stamps (below)
+// The sweep's work units: one per (pair, 256-row query block) that holds query rows of a pair
+// whose target image has keypoints, in pair order: units[0] = their number U, units[1 + u] =
+// p | block << 20.  The sweep gives each XCD a contiguous run of ceil(U / 8) of them (below), so
+// every XCD gets the same number of workgroups and a pair's blocks still share one L2.  (The
+// grid is sized on the host for the capacity, P x ceil(cap / 256) slots; per-pair block counts
+// live on the device.)
+__global__ void __launch_bounds__(1024) k_match_units(const int32_t* __restrict__ count,
+                                                      const int32_t* __restrict__ pairs, int P, int max_rows,
+                                                      int32_t* __restrict__ units) {
+  __shared__ uint32_t s_w[16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  uint32_t base = 0;
+  for (int c0 = 0; c0 < P; c0 += 1024) {
+    const int p = c0 + tid;
+    uint32_t q = 0;
+    if (p < P) {
+      const int n1 = min(count[pairs[2 * p]], max_rows), n2 = count[pairs[2 * p + 1]];
+      q = (n1 > 0 && n2 > 0) ? (uint32_t)((n1 + kQB - 1) / kQB) : 0u;
+    }
+    const uint32_t x = wave_inclusive_scan(q);
+    if (lane == 63) s_w[wid] = x;
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+    for (int w = 0; w < 16; ++w) {
+      const uint32_t t = s_w[w];
+      before += w < wid ? t : 0u;
+      tot += t;
+    }
+    const uint32_t first = base + before + x - q;
+    for (uint32_t j = 0; j < q; ++j) units[1 + first + j] = (int32_t)((uint32_t)p | (j << 20));
+    base += tot;
+    __syncthreads();
+  }
+  if (tid == 0) units[0] = (int32_t)base;
+}
+
+// ABL & 32 (diagnostic build): per-wave shader-clock stamps of the first kStampSt stages of
+// workgroups 0 .. kStampWg-1 (after the stage barrier, after each sub-tile region, after the
+// DMA issue), kept in LDS and copied out at the end (sfm_debug_match_stamps)
+constexpr int kStampWg = 16, kStampSt = 40;
+__device__ uint64_t g_match_stamps[kStampWg][kWaves][kStampSt + 1][4];
+// and for every workgroup of the launch (up to kStampAll): start / end realtime, __smid(),
+// pair | row0 << 32 (0 for workgroups that exit at once)
+constexpr int kStampAll = 1024;
+__device__ uint64_t g_match_wg[kStampAll][4];
+
 template <int STAGE, int ABL = 0>
 __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
     const int32_t* __restrict__ count, int64_t capP, const _Float16* __restrict__ hi,
     const _Float16* __restrict__ lo, const float* __restrict__ norm2, const float* __restrict__ rnorm,
     const float2* __restrict__ pmax, const int32_t* __restrict__ pairs, int P, int max_rows,
     uint32_t* __restrict__ cand, int32_t* __restrict__ cand_n, float* __restrict__ cand_thr,
-    int* __restrict__ ovf_count, int2* __restrict__ ovf_list) {
+    int* __restrict__ ovf_count, int2* __restrict__ ovf_list, const int32_t* __restrict__ units) {
   constexpr bool DMA = STAGE == 1;
   constexpr int NBUF = DMA ? kDmaBufs : kRegBufs;
   constexpr int NNB = DMA ? kDmaNormBufs : kRegNormBufs;
@@ -226,18 +273,44 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   __shared__ __attribute__((aligned(16))) unsigned char smem[kSweepLds];
   float* const sNb = reinterpret_cast<float*>(smem + OFF_N);  // [NNB][kTT2]
   float* const sDb = reinterpret_cast<float*>(smem + OFF_D);  // [kWaves][8][64] float2
+  constexpr bool STAMP = (ABL & 32) != 0;
+  __shared__ uint64_t s_stamp[STAMP ? kWaves * (kStampSt + 1) * 4 : 1];
+  auto stamp = [&](int st, int k) {
+    if constexpr (STAMP) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      if ((threadIdx.x & 63) == 0 && st < kStampSt) s_stamp[((threadIdx.x >> 6) * (kStampSt + 1) + st) * 4 + k] = t;
+    }
+  };
 
   // XCD-aware mapping (workgroups b and b + 8 share an XCD and its L2): group g = b % 8
   // takes the pairs p = g (mod 8), so all query blocks of a pair stream its target table
   // through one L2
   const int QB = (max_rows + kQB - 1) / kQB;
+  if constexpr ((ABL & 32) != 0) {
+    if (threadIdx.x == 0 && blockIdx.x < kStampAll) {
+      g_match_wg[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
+      g_match_wg[blockIdx.x][1] = 0;
+      g_match_wg[blockIdx.x][2] = (uint64_t)__smid();
+      g_match_wg[blockIdx.x][3] = 0;
+    }
+  }
   const int grp = blockIdx.x & 7, slot8 = blockIdx.x >> 3;
-  const int p = grp + 8 * (slot8 / QB);
-  if (p >= P) return;
+  int p, row0;
+  if (units) {  // XCD grp takes units [grp * cu, grp * cu + cu) (k_match_units)
+    const int U = units[0], cu = (U + 7) >> 3;
+    const int u = grp * cu + slot8;
+    if (slot8 >= cu || u >= U) return;
+    const int code = units[1 + u];
+    p = code & 0xFFFFF;
+    row0 = (code >> 20) * kQB;
+  } else {  // SFMFEAT_MATCH_UNITS=0: pairs p = grp (mod 8) on XCD grp, every block slot (A/B)
+    p = grp + 8 * (slot8 / QB);
+    row0 = (slot8 % QB) * kQB;
+    if (p >= P) return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
   const int n1 = count[i1], n2 = count[i2];
-  const int row0 = (slot8 % QB) * kQB;
   if (row0 >= n1 || n2 < 1) return;
 
   // this lane's query row (column of the MFMA output) and its fragments, kept in registers
@@ -359,10 +432,15 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   // ahh, hi.lo + lo.hi into ax (one accumulation chain each)
   auto mfma_sub = [&](const int (&vb)[8], int sub, f32x16& ahh, f32x16& ax) {
     if constexpr ((ABL & 2) != 0) return;
+    h8 t0h, t0l;
+    if constexpr ((ABL & 16) != 0) {
+      t0h = *reinterpret_cast<const h8*>(smem + vb[0] + sub * 32 * ROWB);
+      t0l = *reinterpret_cast<const h8*>(smem + vb[0] + sub * 32 * ROWB + ARRB);
+    }
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-      const h8 thi = *reinterpret_cast<const h8*>(smem + vb[kk] + sub * 32 * ROWB);
-      const h8 tlo = *reinterpret_cast<const h8*>(smem + vb[kk] + sub * 32 * ROWB + ARRB);
+      const h8 thi = (ABL & 16) ? t0h : *reinterpret_cast<const h8*>(smem + vb[kk] + sub * 32 * ROWB);
+      const h8 tlo = (ABL & 16) ? t0l : *reinterpret_cast<const h8*>(smem + vb[kk] + sub * 32 * ROWB + ARRB);
       // k-step 0 starts both chains from an inline-constant zero accumulator
       ahh = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qhi[kk], kk == 0 ? f32x16{} : ahh, 0, 0, 0);
       ax = __builtin_amdgcn_mfma_f32_32x32x16_f16(thi, qlo[kk], kk == 0 ? f32x16{} : ax, 0, 0, 0);
@@ -490,10 +568,18 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   f32x16 hA = {}, xA = {}, hB = {}, xB = {};
   int nbc = 0;                   // norm buffer of stage st (st % NNB)
   int buf = 0;                   // stage buffer of stage st (st % NBUF)
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      s_stamp[(wid * (kStampSt + 1) + kStampSt) * 4 + 0] = __builtin_amdgcn_s_memtime();
+      s_stamp[(wid * (kStampSt + 1) + kStampSt) * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+      s_stamp[(wid * (kStampSt + 1) + kStampSt) * 4 + 3] = (uint64_t)p | ((uint64_t)nst << 32);
+    }
+  }
   for (int st = 0; st < nst; ++st) {
     // stage st is visible, and every wave is done with stage st - 1 (DMA: st - 1's buffer
     // takes stage st + 2 at the end of this iteration; registers: stage st + 1): one barrier
     stage_barrier();
+    stamp(st, 0);
     const int nbp = nbc == 0 ? NNB - 1 : nbc - 1, nbn = nbc == NNB - 1 ? 0 : nbc + 1;
     float nrm_next = 0.0f;
     if constexpr (!DMA) {  // next stage's rows (the last stage re-reads itself: branch-free body)
@@ -514,6 +600,7 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
       pin(b1, b2, mm);
       append(mm, d, (st - 1) * kTT2 + 32);
     }
+    stamp(st, 1);
     {
       float nb[16], d[16];
       uint32_t mm = 0;
@@ -524,6 +611,7 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
       pin(b1, b2, mm);
       append(mm, d, st * kTT2);
     }
+    stamp(st, 2);
     {  // the wave-merged running threshold for the next stage (both halves of a row)
       const float ob1 = other_half(b1), ob2 = other_half(b2);
       thr_w = fminf(fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + E2, thr_w);
@@ -538,6 +626,7 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
       store_stage(buf ^ 1);
       if (tid < kTT2) sNb[nbn * kTT2 + tid] = nrm_next;
     }
+    stamp(st, 3);
     nbc = nbn;
     buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
@@ -549,6 +638,19 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
     append(mm, d, (nst - 1) * kTT2 + 32);
   }
   if constexpr (DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA in flight at exit
+  if constexpr (STAMP) {
+    if (tid == 0 && blockIdx.x < kStampAll) {
+      g_match_wg[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+      g_match_wg[blockIdx.x][3] = (uint64_t)p | ((uint64_t)row0 << 32);
+    }
+    if (lane == 0) s_stamp[(wid * (kStampSt + 1) + kStampSt) * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+    if (blockIdx.x < kStampWg) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // the stamps in LDS (lgkmcnt 0)
+      const uint64_t* src = s_stamp + wid * (kStampSt + 1) * 4;
+      uint64_t* dst = &g_match_stamps[blockIdx.x][wid][0][0];
+      for (int i = lane; i < (kStampSt + 1) * 4; i += 64) dst[i] = src[i];
+    }
+  }
   // the row's final window threshold (both halves merged): the re-rank drops the admitted
   // targets above it (their stored d~ is rounded down, so no window member is dropped)
   const float ob1 = other_half(b1), ob2 = other_half(b2);
@@ -936,6 +1038,8 @@ __global__ void __launch_bounds__(256) k_match_overflow(const float* __restrict_
   }
 }
 
+size_t match_units_words(int P, int max_rows) { return 1 + (size_t)P * ((max_rows + kQB - 1) / kQB); }
+
 size_t match_pmax_bytes(int64_t capP) { return (size_t)(capP / kPrepRows) * sizeof(float2); }
 
 void launch_match_prep(const float* desc, const int32_t* count, int nimg, int64_t cap, int64_t capP,
@@ -948,7 +1052,7 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
                        const _Float16* hi, const _Float16* lo, const float* norm2, const float* rnorm,
                        const void* pmax, const int32_t* pairs, int P, float ratio,
                        RowBest* rows, int max_rows, uint32_t* cand, int32_t* cand_n, float* cand_thr,
-                       int* ovf_count, int2* ovf_list, hipStream_t st) {
+                       int* ovf_count, int2* ovf_list, int32_t* units, hipStream_t st) {
   static const int stage = [] {  // SFMFEAT_MATCH_STAGE=reg: register-staged sweep (A/B timing)
     const char* e = getenv("SFMFEAT_MATCH_STAGE");
     return (e && e[0] == 'r') ? 0 : 1;
@@ -957,13 +1061,19 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
     const char* e = getenv("SFMFEAT_RERANK8_MAX");
     return e ? atoi(e) : kRerank8MaxPairs;
   }();
+  static const bool use_units = [] {  // SFMFEAT_MATCH_UNITS=0: the per-pair XCD mapping (A/B)
+    const char* e = getenv("SFMFEAT_MATCH_UNITS");
+    return !(e && e[0] == '0');
+  }();
   const int qb = (max_rows + kQB - 1) / kQB;
   const dim3 grid((unsigned)(8 * ((P + 7) / 8) * qb));
+  if (!use_units) units = nullptr;
+  if (units) hipLaunchKernelGGL(k_match_units, dim3(1), dim3(1024), 0, st, count, pairs, P, max_rows, units);
   // ovf_count is zero here: set once at allocation, re-zeroed by k_match_compact
 #define SFM_SWEEP(A, ABL)                                                                             \
   hipLaunchKernelGGL((k_match_mfma<A, ABL>), grid, dim3(kNT), 0, st, count, capP, hi, lo, norm2, rnorm,   \
                      static_cast<const float2*>(pmax), pairs, P, max_rows, cand, cand_n, cand_thr, ovf_count, \
-                     ovf_list)
+                     ovf_list, units)
   static const int abl = [] {  // timing ablations: diagnostic build only (SFM_ABLATION_ENV)
     const char* e = SFM_ABLATION_ENV("SFMFEAT_MATCH_ABL");
     return e ? atoi(e) : 0;
@@ -975,6 +1085,9 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
     case 3: SFM_SWEEP(1, 3); break;
     case 4: SFM_SWEEP(1, 4); break;
     case 6: SFM_SWEEP(1, 6); break;
+    case 16: SFM_SWEEP(1, 16); break;
+    case 17: SFM_SWEEP(1, 17); break;
+    case 32: SFM_SWEEP(1, 32); break;
     default: if (stage == 0) SFM_SWEEP(0, 0); else SFM_SWEEP(1, 0);
   }
 #else
@@ -1003,6 +1116,23 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
   // the overflow list's length stays on the device: a fixed grid strides over it
   hipLaunchKernelGGL(k_match_overflow, dim3(256), dim3(256), 0, st, desc, count, cap, pairs, ratio, rows, max_rows,
                      ovf_count, ovf_list);
+}
+
+// the sweep's clock stamps of its last SFMFEAT_MATCH_ABL=32 launch (diagnostic build): u64
+// [kStampWg][kWaves][kStampSt + 1][4], then [kStampAll][4]; returns the slots copied, -1 in
+// the shipped build
+int64_t match_stamps_copy(uint64_t* out, int64_t cap) {
+#ifdef SFM_ABLATIONS
+  const int64_t n1 = (int64_t)sizeof(g_match_stamps) / 8, n = n1 + (int64_t)sizeof(g_match_wg) / 8;
+  if (cap < n) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_match_stamps), sizeof(g_match_stamps)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out + n1, HIP_SYMBOL(g_match_wg), sizeof(g_match_wg)) != hipSuccess) return -1;
+  return n;
+#else
+  (void)out;
+  (void)cap;
+  return -1;
+#endif
 }
 
 }  // namespace sfm

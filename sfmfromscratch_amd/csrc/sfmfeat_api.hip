@@ -65,7 +65,7 @@ struct sfm_ctx {
   DevBuf d_gauss, d_img0, d_lvl, d_R, d_hist, d_med, d_medlist, d_counts, d_cand, d_scratch,
       d_kpx, d_kpy, d_kpc, d_lc, d_xy, d_desc, d_conf, d_count, d_u8;
   DevBuf m_desc, m_count, m_pairs, m_descT, m_rows, m_matches, m_conf, m_nmatch;
-  DevBuf m_hi, m_lo, m_norm2, m_rnorm, m_imgmax, m_ovf, m_ovfc, m_cand, m_candn, m_candt;
+  DevBuf m_hi, m_lo, m_norm2, m_rnorm, m_imgmax, m_ovf, m_ovfc, m_cand, m_candn, m_candt, m_units;
   // ingest (sfm_ingest_rgb*): resample tables for the cached (W -> W2, H -> H2) and the
   // RGB temp of the horizontal pass; host staging for the host-pointer variant
   DevBuf i_tab_h, i_tab_v, i_tmp, i_rgb, i_gray;
@@ -604,6 +604,7 @@ int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, in
     if ((rc = ensure(c, c->m_cand, (size_t)Pmax * cap * kMatchCandCap * 4))) return rc;
     if ((rc = ensure(c, c->m_candn, (size_t)Pmax * cap * 4))) return rc;
     if ((rc = ensure(c, c->m_candt, (size_t)Pmax * cap * 4))) return rc;
+    if ((rc = ensure(c, c->m_units, match_units_words(Pmax, (int)cap) * 4))) return rc;
   }
   for (int p0 = 0; p0 < P; p0 += Pmax, ++c->match_calls) {
     const int Pn = std::min(Pmax, P - p0);
@@ -618,7 +619,7 @@ int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, in
       if (!(c->match_calls > 0 && (skip_mask() & 8))) launch_match_mfma(desc, count, cap, capP, as<_Float16>(c->m_hi), as<_Float16>(c->m_lo), as<float>(c->m_norm2),
                         as<float>(c->m_rnorm), c->m_imgmax.p, pr, Pn, ratio, as<RowBest>(c->m_rows),
                         (int)cap, as<uint32_t>(c->m_cand), as<int32_t>(c->m_candn), as<float>(c->m_candt),
-                        as<int>(c->m_ovfc), as<int2>(c->m_ovf), st);
+                        as<int>(c->m_ovfc), as<int2>(c->m_ovf), as<int32_t>(c->m_units), st);
     }
     {
       StageScope sc(c, SFM_PROF_MATCH_POST, st);
@@ -760,7 +761,7 @@ int32_t sfm_ctx_destroy(sfm_ctx* c) {
                     &c->d_counts, &c->d_cand, &c->d_scratch, &c->d_kpx, &c->d_kpy, &c->d_kpc, &c->d_lc,
                     &c->d_xy, &c->d_desc, &c->d_conf, &c->d_count, &c->d_u8, &c->m_desc, &c->m_count, &c->m_pairs,
                     &c->m_descT, &c->m_rows, &c->m_matches, &c->m_conf, &c->m_nmatch,
-                    &c->m_hi, &c->m_lo, &c->m_norm2, &c->m_rnorm, &c->m_imgmax, &c->m_ovf, &c->m_ovfc, &c->m_cand, &c->m_candn, &c->m_candt,
+                    &c->m_hi, &c->m_lo, &c->m_norm2, &c->m_rnorm, &c->m_imgmax, &c->m_ovf, &c->m_ovfc, &c->m_cand, &c->m_candn, &c->m_candt, &c->m_units,
                     &c->i_tab_h, &c->i_tab_v, &c->i_tmp, &c->i_rgb, &c->i_gray, &c->i_colmap, &c->i_sets,
                     &c->r_idx, &c->r_off, &c->r_F, &c->r_counts, &c->r_pts, &c->r_npts, &c->r_out, &c->r_on,
                     &c->r_oit};

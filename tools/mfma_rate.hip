@@ -2,7 +2,9 @@
 // per k-step three MFMAs (hi.hi into one accumulator, hi.lo + lo.hi into another) — at 1 and 2
 // waves per SIMD, with the target fragments (a) in registers, (b) read from LDS one k-step
 // ahead (two ds_read_b128 per k-step, as k_match_mfma does).  Prints cycles per MFMA per SIMD.
-// Usage: mfma_rate [iters]
+// With rnd = 1 every operand is a pseudo-random f16 of descriptor-like magnitude (full mantissa
+// toggling) instead of the few repeated values of rnd = 0: the matcher's operands are random.
+// Usage: mfma_rate [iters] [rnd]
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -10,17 +12,28 @@
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+__device__ inline _Float16 rnd_h(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return (_Float16)(0.25f + (float)(x & 0xffffff) * (1.0f / 16777216.0f) * 63.0f);  // [0.25, 63.25)
+}
+
 template <int MODE>
-__global__ void __launch_bounds__(256) k_rate(float* out, int iters, unsigned long long* cyc) {
+__global__ void __launch_bounds__(256) k_rate(float* out, int iters, unsigned long long* cyc, int rnd) {
   __shared__ __attribute__((aligned(16))) _Float16 s_t[2][64 * 136];
   const int lane = threadIdx.x & 63;
-  for (int i = threadIdx.x; i < 2 * 64 * 136; i += 256) (&s_t[0][0])[i] = (_Float16)(0.001f * (i & 63));
+  for (int i = threadIdx.x; i < 2 * 64 * 136; i += 256)
+    (&s_t[0][0])[i] = rnd ? rnd_h(i * 2654435761u + 17) : (_Float16)(0.001f * (i & 63));
   __syncthreads();
   h8 q[8], t[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     q[k] = h8{(_Float16)(0.01f * k), 1, 2, 3, 4, 5, 6, (_Float16)lane};
     t[k] = h8{(_Float16)(0.02f * k), 2, 1, 3, 5, 4, 6, (_Float16)lane};
+    if (rnd)
+      for (int e = 0; e < 8; ++e) {
+        q[k][e] = rnd_h((lane * 64 + k * 8 + e) * 40503u + blockIdx.x);
+        t[k][e] = rnd_h((lane * 64 + k * 8 + e) * 9973u + 7 * blockIdx.x + 1);
+      }
   }
   f32x16 a = {}, x = {};
   const unsigned long long c0 = __builtin_amdgcn_s_memtime();
@@ -52,13 +65,16 @@ __global__ void __launch_bounds__(256) k_rate(float* out, int iters, unsigned lo
   if (lane == 0) cyc[blockIdx.x * 4 + (threadIdx.x >> 6)] = c1 - c0;
 }
 
+static int g_rnd = 0;
 template <int MODE>
 static void launch(dim3 grid, float* out, int iters, unsigned long long* cyc) {
-  hipLaunchKernelGGL(k_rate<MODE>, grid, dim3(256), 0, 0, out, iters, cyc);
+  hipLaunchKernelGGL(k_rate<MODE>, grid, dim3(256), 0, 0, out, iters, cyc, g_rnd);
 }
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 4000;
+  g_rnd = argc > 2 ? atoi(argv[2]) : 0;
+  printf("operands: %s\n", g_rnd ? "pseudo-random f16" : "repeated values");
   float* out;
   (void)hipMalloc(&out, 4);
   unsigned long long* cyc;
