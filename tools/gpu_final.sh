@@ -2,10 +2,13 @@
 # End-of-round evidence on one GPU: GPU suite, smoke, the driver's bench command three times,
 # the other BASELINE configs, a rocprofv3 kernel trace of the headline bench, HBM traffic and SQ
 # counter passes, and the N = 2 launcher rehearsal over gloo.  Outputs: gpurun_out/<TAG>_*.
+# PHASE=1: tests, smoke and the benches; PHASE=2: trace, PMC passes, rehearsal (one gpurun call
+# each fits its time limit); unset: everything.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-T=${TAG:-r04_final}
+T=${TAG:-r05_final}
+PH=${PHASE:-0}
 O=gpurun_out
 mkdir -p $O
 step() {  # step NAME SECONDS CMD...
@@ -15,6 +18,7 @@ step() {  # step NAME SECONDS CMD...
   local rc=$?
   [ $rc -eq 0 ] || { echo "$name rc=$rc"; tail -20 "$O/${T}_$name.err" "$O/${T}_$name.out"; exit $rc; }
 }
+if [ "$PH" != 2 ]; then
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
   step pytest_gpu 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread
   tail -1 $O/${T}_pytest_gpu.out
@@ -29,6 +33,8 @@ step bench_c3 300 python bench.py --workload c3 --steps 5 --warmup 2 --cpu-sampl
 step bench_c4 300 python bench.py --workload c4 --steps 5 --warmup 2 --cpu-sample 0 --verify
 step bench_c5 300 python bench.py --workload c5 --steps 100 --warmup 5 --cpu-sample 0
 for w in c3 c4 c5; do python -c "import json;d=json.load(open('$O/${T}_bench_$w.out'));print('$w', d['value'], d['ms_per_step'])"; done
+fi
+[ "$PH" = 1 ] && { echo done; exit 0; }
 step trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_prof -o run -- python bench.py --steps 20 --warmup 5 --cpu-sample 0 --no-profile
 python tools/trace_summary.py $O/${T}_prof > $O/${T}_trace_summary.txt
 for c in FETCH_SIZE WRITE_SIZE; do
