@@ -822,12 +822,14 @@ __global__ void __launch_bounds__(256) k_match_rerank2(const float* __restrict__
   for (int s0 = 0; s0 < nkmax; s0 += 4) {
     const int sidx = s0 + grp;
     const bool okc = sidx < nk;
+    // j = 0 for the group's idle lanes: a valid row (of image 0 for an idle item), whose
+    // distance is computed and never used, so the loads need no lane masks
     const int j = okc ? (int)sJ[wv][hf][sidx] : 0;
     const float* b = Bd + (int64_t)j * 128;
     float r = 0.0f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float dd = a[i] - (okc ? b[8 * i + l8] : a[i]);
+      const float dd = a[i] - b[8 * i + l8];
       const float sq = dd * dd;
       r = (i == 0) ? sq : r + sq;
     }

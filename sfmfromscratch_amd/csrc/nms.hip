@@ -317,6 +317,11 @@ __global__ void __launch_bounds__(NT) k_nms_band(const float* __restrict__ R, co
   const int b = blockIdx.y;
   if (st[b].fallback != 0) return;  // whole workgroup: fallback planes take the exact path
   const uint32_t tnms = st[b].tnms;
+  // fkey(v) >= tnms as one float compare v >= T: fkey is a monotone bijection between the
+  // non-NaN floats (-0 folded onto +0, as IEEE compares them) and the keys 0x007FFFFF ..
+  // 0xFF800000, so T = fkey_inv(tnms) inside that range, -inf below it (every value passes)
+  // and NaN above it (none does)
+  const float T = tnms <= 0x007FFFFFu ? -INFINITY : tnms > 0xFF800000u ? __uint_as_float(0x7FC00000u) : fkey_inv(tnms);
   const int64_t n = (int64_t)H * W;
   const float* Rp = R + (int64_t)b * n;
   const int C4 = W >> 2;
@@ -336,9 +341,13 @@ __global__ void __launch_bounds__(NT) k_nms_band(const float* __restrict__ R, co
     const int eoff = need_l ? -1 : 4;
     // one image row of this column group: its 4 values (-inf outside the image) and the
     // horizontal max3 of each column (outer neighbours from the adjacent lanes / the edge load)
+    // (rowok is a compile-time true for bands whose every row lies inside the image)
     auto hrow = [&](const float4& v0, float e, bool rowok, float4& v, float (&h)[4]) {
       v = rowok ? v0 : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-      const float up = __shfl_up(v.w, 1), dn = __shfl_down(v.x, 1);
+      // lane - 1's v.w and lane + 1's v.x by DPP wave_shr:1 / wave_shl:1 (no LDS round trip;
+      // lane 0's up and lane 63's dn are never used: they take e or -inf)
+      const float up = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v.w), 0x138, 0xF, 0xF, false));
+      const float dn = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v.x), 0x130, 0xF, 0xF, false));
       float l = c4 == 0 ? -INFINITY : (lane == 0 ? e : up);
       float r = c4 == C4 - 1 ? -INFINITY : (lane == 63 ? e : dn);
       if (!rowok) l = r = -INFINITY;
@@ -352,6 +361,11 @@ __global__ void __launch_bounds__(NT) k_nms_band(const float* __restrict__ R, co
       v = *reinterpret_cast<const float4*>(colp + (int64_t)gy * W);
       e = (need_l || need_r) ? colp[(int64_t)gy * W + eoff] : -INFINITY;
     };
+    uint64_t flags0 = 0ull, flags1 = 0ull;
+    // IN: every image row the band reads (ytop - 1 .. ytop + NB * SH) lies inside the image,
+    // so no row needs its -inf fill and every output row is inside
+    auto band_body = [&](auto inc) {
+    constexpr bool IN = decltype(inc)::value;
     // carried rows: a = row y - 1, c = row y (values and horizontal maxima)
     float4 va, vc;
     float ha[4], hc[4];
@@ -360,10 +374,9 @@ __global__ void __launch_bounds__(NT) k_nms_band(const float* __restrict__ R, co
       float e0, e1;
       load(ytop - 1, r0, e0);
       load(ytop, r1, e1);
-      hrow(r0, e0, ytop - 1 >= 0 && ytop - 1 < H, va, ha);
-      hrow(r1, e1, ytop < H, vc, hc);
+      hrow(r0, e0, IN || (ytop - 1 >= 0 && ytop - 1 < H), va, ha);
+      hrow(r1, e1, IN || ytop < H, vc, hc);
     }
-    uint64_t flags0 = 0ull, flags1 = 0ull;
 #pragma unroll 1
     for (int sb = 0; sb < NB; ++sb) {  // not unrolled: one strip's registers at a time
       const int y0 = ytop + sb * SH;  // output rows y0 .. y0 + 7 need image rows up to y0 + 8
@@ -377,16 +390,16 @@ __global__ void __launch_bounds__(NT) k_nms_band(const float* __restrict__ R, co
         float4 vn;
         float hn[4];
         const int yn = y0 + 1 + j;
-        hrow(raw[j], er[j], yn < H, vn, hn);
+        hrow(raw[j], er[j], IN || yn < H, vn, hn);
         // output row y = yn - 1: centre vc, window rows a (y - 1), c (y), n (y + 1)
         const int y = yn - 1;
-        const bool inside = active && y < H;
+        const bool inside = active && (IN || y < H);
         const float cv[4] = {vc.x, vc.y, vc.z, vc.w};
         uint32_t fr = 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float m = fmaxf(fmaxf(ha[e], hc[e]), hn[e]);
-          const bool pred = inside && fkey(cv[e]) >= tnms && cv[e] == m;
+          const bool pred = inside && cv[e] >= T && cv[e] == m;
           fr |= pred ? (1u << (4 * j + e)) : 0u;
         }
         strip |= fr;
@@ -402,6 +415,9 @@ __global__ void __launch_bounds__(NT) k_nms_band(const float* __restrict__ R, co
       if (sb < 2) flags0 |= sw;
       else flags1 |= sw;
     }
+    };
+    if (ytop >= 1 && ytop + NB * SH <= H - 1) band_body(std::true_type{});
+    else band_body(std::false_type{});
     const uint64_t flags[2] = {flags0, flags1};
     const uint32_t nf = (uint32_t)(__popcll(flags[0]) + __popcll(flags[1]));
     if (!__syncthreads_or(nf != 0)) continue;

@@ -391,6 +391,52 @@ def test_configs2_workload_1080p_all_pairs_vs_oracle():
         assert_matches_equal(om[p][0], om[p][1], mm[p, :k], mc[p, :k])
 
 
+def test_matcher_work_units_ragged_counts_many_pairs():
+    """The sweep's work units (k_match_units): ragged per-image counts around the 256-row
+    query blocks (0, 1, 255, 256, 257, 511, 513, ...), so pairs have 0-3 blocks and some none,
+    and 1,128 pairs (the unit scan's second 1,024-pair chunk); every pair equals the oracle
+    (n2 < 2: the reference's IndexError, nmatch -1)."""
+    torch = pytest.importorskip("torch")
+    from sfmfromscratch_amd.pipeline import BatchMatcher, SlotTable, all_pairs
+    ns = [0, 1, 2, 255, 256, 257, 300, 511, 513, 700, 64, 129, 400, 5, 260, 768]
+    S, cap = 48, 768
+    counts = [ns[i % len(ns)] for i in range(S)]
+    base, hb = synth.make_descriptor_table(cap, 4242)
+    slots = SlotTable(torch, S, cap, "cuda")
+    host = np.zeros((S, cap, 128), np.float32)
+    for i, n in enumerate(counts):
+        if n:
+            t, _ = synth.make_descriptor_table(n, 5000 + i, dup_of=hb[:n] if i % 3 else None, jitter=2)
+            host[i, :n] = t
+    slots.desc.copy_(torch.from_numpy(host))
+    slots.count.copy_(torch.tensor(counts, dtype=torch.int32))
+    pairs_np = all_pairs(S)
+    assert len(pairs_np) > 1024
+    mm, mc, nm = BatchMatcher(0.85).match(slots, torch.from_numpy(pairs_np).cuda())
+    torch.cuda.synchronize()
+    mm, mc, nm = mm.cpu().numpy(), mc.cpu().numpy(), nm.cpu().numpy()
+
+    def ref(pq):
+        i, j = pq
+        try:
+            return O.match(host[i, :counts[i]], host[j, :counts[j]], 0.85)
+        except IndexError:
+            return None
+
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(16) as pool:
+        refs = list(pool.map(ref, [tuple(p) for p in pairs_np]))
+    for p, (i, j) in enumerate(pairs_np):
+        if refs[p] is None:
+            assert nm[p] == -1, (i, j, counts[i], counts[j], nm[p])
+            continue
+        om, oc = refs[p]
+        k = int(nm[p])
+        assert k == len(oc), (i, j, counts[i], counts[j], k, len(oc))
+        if k:
+            assert_matches_equal(om, oc, mm[p, :k], mc[p, :k])
+
+
 def test_prep_ranges_then_prepped_match_equal_full_match():
     """sfm_match_prep_dev over slot ranges + sfm_match_pairs_prepped_dev (the configs[3]
     chunked path) give exactly sfm_match_pairs_dev's results; prepped matching on a fresh
