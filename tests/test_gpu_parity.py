@@ -122,6 +122,24 @@ def test_extract_and_match_vs_golden_and_oracle(name):
         assert a == b, (len(a), len(b), len(a ^ b))  # bit-identical pairs (north_star)
 
 
+@pytest.mark.parametrize("name", ["extract_small_pmain_stablehist.npz", "extract_small_scalerot_stablehist.npz"])
+def test_descriptors_vs_reference_stable_histogram_no_escape(name):
+    """Against the reference run with a stable np.histogram sort (its tie order = ours): every
+    descriptor element within 5e-7 absolute, no near-empty-bin escape."""
+    z = load(name)
+    H, W, seed, nframes, stride = (int(v) for v in z["meta"])
+    pp = params_of(z)
+    for f in range(nframes):
+        img = frame(H, W, seed, f, z[f"f{f}_sha"])
+        obj = ScaleRotInvSIFT(img, pp)
+        X, Y = obj.detect_keypoints()
+        D = obj.extract_descriptors()
+        perm = tie_permutation(z[f"f{f}_X"], z[f"f{f}_Y"], X, Y, obj.confidences)
+        ref = z[f"f{f}_D"]
+        assert desc_close(ref, D[perm][::stride], rtol=0.0, atol=5e-7, max_escapes=0), \
+            float(np.abs(ref - D[perm][::stride]).max())
+
+
 def test_matcher_vs_golden_tables():
     z = load("match.npz")
     for i in range(int(z["ncases"])):

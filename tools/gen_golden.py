@@ -188,6 +188,35 @@ def gen_extract(name, H, W, seed, pp, mode, nframes=2, desc_stride=1, ratio=0.85
     save(name, **out)
 
 
+class _StableSortNumpy:
+    """numpy with a stable argsort, for numpy's histogram module only."""
+
+    def __getattr__(self, name):
+        return getattr(np, name)
+
+    @staticmethod
+    def argsort(a, *args, **kw):
+        kw.pop("kind", None)
+        return np.argsort(a, *args, kind="stable", **kw)
+
+
+def gen_extract_stable_hist(name, H, W, seed, pp, mode, nframes=2):
+    """The reference's extraction with np.histogram's weighted path sorting STABLY (ties of
+    equal orientations summed in window raster order).  numpy's default argsort is unstable,
+    so which order a tie's weights are summed in is CPU-specific and a near-empty bin (a
+    difference of two float32 prefix sums) can move by a few ulp of the running total; with a
+    stable sort the reference's descriptors are fully determined, and tests compare them
+    without the near-empty-bin escape (tests/golden_util.desc_close max_escapes=0).  Only
+    the histogram module's numpy is replaced; keypoint selection is untouched."""
+    import numpy.lib._histograms_impl as hist_impl
+    saved = hist_impl.np
+    hist_impl.np = _StableSortNumpy()
+    try:
+        gen_extract(name, H, W, seed, pp, mode, nframes=nframes)
+    finally:
+        hist_impl.np = saved
+
+
 def gen_match():
     out = {}
     cases = []
@@ -298,6 +327,10 @@ def main():
                           gen_extract("extract_small_naive.npz", 150, 200, 23, {"num_interest_points": 500},
                                       "naive", ratio=0.8),
                           gen_extract("extract_small_defaults.npz", 128, 160, 24, {}, "scalerot")),
+        "stable": lambda: (gen_extract_stable_hist("extract_small_pmain_stablehist.npz", 151, 203, 22, P_MAIN,
+                                                   "scalerot"),
+                           gen_extract_stable_hist("extract_small_scalerot_stablehist.npz", 150, 200, 21, P_OCT,
+                                                   "scalerot")),
         "c1": lambda: gen_extract("extract_c1_640x480_pmain.npz", 480, 640, 1234, P_MAIN, "scalerot",
                                   desc_stride=4),
         "c2": lambda: gen_extract("extract_c2_1080p_poct.npz", 1080, 1920, 1234, P_OCT, "scalerot",
