@@ -126,6 +126,16 @@ SFM_DEV uint16_t bf16_down(float v) {
   return v >= 0.0f ? (uint16_t)(__float_as_uint(v) >> 16) : (uint16_t)0xFF80u;
 }
 
+// (m & a) | (~m & b) as one v_bfi_b32 (asm: the compiler turns a select tree over an array
+// back into a dynamically indexed stack array)
+SFM_DEV uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+// all ones when bit `bit` of x is set, else 0 (v_bfe_i32: the bit, sign-extended)
+SFM_DEV uint32_t lane_bit_mask(int x, int bit) { return (uint32_t)__builtin_amdgcn_sbfe(x, bit, 1); }
+
 // x of the lane 32 away (the other half of the wavefront): one v_permlane32_swap + a select,
 // instead of a ds_bpermute through the LDS crossbar
 SFM_DEV float other_half(float x) {
@@ -160,6 +170,15 @@ constexpr size_t kSweepLds = (size_t)kDmaBufs * 2 * kTT2 * 256 + kDmaNormBufs * 
 static_assert(kSweepLds >= (size_t)kRegBufs * 2 * kTT2 * kRowH * 2 + kRegNormBufs * kTT2 * 4 + kDBytes,
               "one LDS array serves both staging forms");
 static_assert(kSweepLds <= 160 * 1024, "LDS per CU");
+// STAGE 3 (the half-CU form): 4 waves x 32 query rows, two LDS-DMA stage buffers, no LDS
+// staging of the appends: 65 KB of LDS and <= 256 VGPRs at one wave per SIMD, so a k_harris
+// workgroup (80 KB, one wave per SIMD) fits beside it on the same CU — the matcher's MFMAs
+// and Harris's VALU then share the SIMDs instead of taking CUs in turn
+constexpr int kWaves3 = 4;
+constexpr size_t kSweepLds3 = (size_t)2 * 2 * kTT2 * 256 + 3 * kTT2 * 4 + 256;
+static_assert(kSweepLds3 + 80 * 1024 <= 160 * 1024, "half-CU sweep beside one Harris workgroup");
+constexpr int sweep_waves(int stage) { return stage == 3 ? kWaves3 : kWaves; }
+constexpr int sweep_rows(int stage) { return kQW * sweep_waves(stage); }
 
 // LDS-DMA (global_load_lds) issued from inline asm, M0 = the wave-uniform LDS destination:
 // hipcc's own waitcnt pass then does not see them (it would wait vmcnt(0) ahead of every LDS
@@ -216,7 +235,7 @@ __device__ __forceinline__ void glds_x1(const void* gsrc, uint32_t lds_dst) {
 // live on the device.)
 __global__ void __launch_bounds__(1024) k_match_units(const int32_t* __restrict__ count,
                                                       const int32_t* __restrict__ pairs, int P, int max_rows,
-                                                      int32_t* __restrict__ units) {
+                                                      int qbr, int32_t* __restrict__ units) {
   __shared__ uint32_t s_w[16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   uint32_t base = 0;
@@ -225,7 +244,7 @@ __global__ void __launch_bounds__(1024) k_match_units(const int32_t* __restrict_
     uint32_t q = 0;
     if (p < P) {
       const int n1 = min(count[pairs[2 * p]], max_rows), n2 = count[pairs[2 * p + 1]];
-      q = (n1 > 0 && n2 > 0) ? (uint32_t)((n1 + kQB - 1) / kQB) : 0u;
+      q = (n1 > 0 && n2 > 0) ? (uint32_t)((n1 + qbr - 1) / qbr) : 0u;
     }
     const uint32_t x = wave_inclusive_scan(q);
     if (lane == 63) s_w[wid] = x;
@@ -255,22 +274,25 @@ constexpr int kStampAll = 1024;
 __device__ uint64_t g_match_wg[kStampAll][4];
 
 template <int STAGE, int ABL = 0>
-__global__ void __launch_bounds__(kNT, 1) k_match_mfma(
+__global__ void __launch_bounds__(64 * sweep_waves(STAGE), STAGE == 3 ? 2 : 1) k_match_mfma(
     const int32_t* __restrict__ count, int64_t capP, const _Float16* __restrict__ hi,
     const _Float16* __restrict__ lo, const float* __restrict__ norm2, const float* __restrict__ rnorm,
     const float2* __restrict__ pmax, const int32_t* __restrict__ pairs, int P, int max_rows,
     uint32_t* __restrict__ cand, int32_t* __restrict__ cand_n, float* __restrict__ cand_thr,
     int* __restrict__ ovf_count, int2* __restrict__ ovf_list, const int32_t* __restrict__ units) {
-  constexpr bool DMA = STAGE == 1;
-  constexpr int NBUF = DMA ? kDmaBufs : kRegBufs;
-  constexpr int NNB = DMA ? kDmaNormBufs : kRegNormBufs;
+  constexpr bool DMA = STAGE >= 1;
+  constexpr bool H3 = STAGE == 3;                // the half-CU form
+  constexpr int NW = sweep_waves(STAGE), NTH = 64 * NW, QBR = sweep_rows(STAGE);
+  constexpr int NBUF = H3 ? 2 : DMA ? kDmaBufs : kRegBufs;
+  constexpr int NNB = H3 ? 3 : DMA ? kDmaNormBufs : kRegNormBufs;
   constexpr int ROWB = DMA ? 256 : kRowH * 2;  // bytes per staged target row
   constexpr int ARRB = kTT2 * ROWB;            // one array (hi or lo) of a stage
   constexpr int BUFB = 2 * ARRB;
   constexpr int OFF_N = NBUF * BUFB;
   constexpr int OFF_D = OFF_N + NNB * kTT2 * 4;
-  static_assert((size_t)OFF_D + kDBytes <= kSweepLds, "LDS carve");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[kSweepLds];
+  constexpr size_t LDSB = H3 ? kSweepLds3 : kSweepLds;
+  static_assert((size_t)OFF_D + (H3 ? 256 : kDBytes) <= LDSB, "LDS carve");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDSB];
   float* const sNb = reinterpret_cast<float*>(smem + OFF_N);  // [NNB][kTT2]
   float* const sDb = reinterpret_cast<float*>(smem + OFF_D);  // [kWaves][8][64] float2
   constexpr bool STAMP = (ABL & 32) != 0;
@@ -285,7 +307,7 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   // XCD-aware mapping (workgroups b and b + 8 share an XCD and its L2): group g = b % 8
   // takes the pairs p = g (mod 8), so all query blocks of a pair stream its target table
   // through one L2
-  const int QB = (max_rows + kQB - 1) / kQB;
+  const int QB = (max_rows + QBR - 1) / QBR;
   if constexpr ((ABL & 32) != 0) {
     if (threadIdx.x == 0 && blockIdx.x < kStampAll) {
       g_match_wg[blockIdx.x][0] = __builtin_amdgcn_s_memrealtime();
@@ -302,10 +324,10 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
     if (slot8 >= cu || u >= U) return;
     const int code = units[1 + u];
     p = code & 0xFFFFF;
-    row0 = (code >> 20) * kQB;
+    row0 = (code >> 20) * QBR;
   } else {  // SFMFEAT_MATCH_UNITS=0: pairs p = grp (mod 8) on XCD grp, every block slot (A/B)
     p = grp + 8 * (slot8 / QB);
-    row0 = (slot8 % QB) * kQB;
+    row0 = (slot8 % QB) * QBR;
     if (p >= P) return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -332,7 +354,7 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   {
     const int nblk = (int)(capP / kPrepRows);
     float m2 = 0.0f, mr = 0.0f;
-    for (int t = tid; t < nblk; t += kNT) {
+    for (int t = tid; t < nblk; t += NTH) {
       const float2 v = pmax[(int64_t)i2 * nblk + t];
       m2 = fmaxf(m2, v.x);
       mr = fmaxf(mr, v.y);
@@ -349,7 +371,7 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
     maxn2 = sDb[0];
     maxrn = sDb[1];
 #pragma unroll
-    for (int w = 1; w < kWaves; ++w) {
+    for (int w = 1; w < NW; ++w) {
       maxn2 = fmaxf(maxn2, sDb[2 * w]);
       maxrn = fmaxf(maxrn, sDb[2 * w + 1]);
     }
@@ -384,10 +406,30 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
     }
     if (wid_u == 0) glds_x1(nrm_t + rb + lane, smem_lds + (uint32_t)(OFF_N + nbuf * kTT2 * 4));
   };
+  // STAGE 3: a stage's 32 pieces over 4 waves: wave w fetches chunks 4 k + w (k = 0..3) of
+  // both arrays, in two parts (one per sub-tile region; part 0 also carries wave 0's norms)
+  auto issue_part3 = [&](int stg, int buf, int nbuf, int part) {
+    const int64_t rb = (int64_t)stg * kTT2;  // rows < capP: in bounds
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = 4 * part + jj;
+      const int a = j >> 2, ci = 4 * (j & 3) + wid, ciu = 4 * (j & 3) + wid_u;
+      const int row = 4 * ci + (lane >> 4);
+      const int c = (lane & 15) ^ (row & 15);
+      const _Float16* src = (a ? lo : hi) + to + (rb + row) * 128 + c * 8;
+      glds_x4(src, smem_lds + (uint32_t)(buf * BUFB + a * ARRB + ciu * 1024));
+    }
+    if (part == 0 && wid_u == 0) glds_x1(nrm_t + rb + lane, smem_lds + (uint32_t)(OFF_N + nbuf * kTT2 * 4));
+  };
   // this wave's share of the stage issued two iterations ago has landed (the last stage's
   // share stays in flight); then every wave's
   auto stage_barrier = [&]() {
-    if constexpr (DMA) {
+    if constexpr (H3) {  // this wave's pieces of stage st (issued one stage ago) have landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else if constexpr (DMA) {
       if (wid_u == 0) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -529,7 +571,25 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
   // conflict at most 2-way (a lane-major [lane][16] row put 4 lanes on the same banks)
   float2* const my_d2 = reinterpret_cast<float2*>(sDb) + wid * 8 * 64 + lane;
   auto append = [&](uint32_t mm, const float (&d)[16], int jb) {
-    if (__any(mm != 0u)) {  // wave-uniform: skip when no lane admits
+    if constexpr (H3) {  // no LDS staging: d[rr] by a 4-level v_bfi_b32 select tree
+      if (live) {
+        for (; mm; mm &= mm - 1, ++cnt) {
+          const int rr = __builtin_ctz(mm);
+          uint32_t a8[8], a4[4], a2[2];
+          const uint32_t m0 = lane_bit_mask(rr, 0), m1 = lane_bit_mask(rr, 1), m2 = lane_bit_mask(rr, 2),
+                         m3 = lane_bit_mask(rr, 3);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a8[i] = bfi(m0, __float_as_uint(d[2 * i + 1]), __float_as_uint(d[2 * i]));
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a4[i] = bfi(m1, a8[2 * i + 1], a8[2 * i]);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) a2[i] = bfi(m2, a4[2 * i + 1], a4[2 * i]);
+          const float dr = __uint_as_float(bfi(m3, a2[1], a2[0]));
+          if (cnt < kHalfCap)
+            my_list[cnt] = (uint32_t)(jb + 4 * half + (rr & 3) + 8 * (rr >> 2)) | ((uint32_t)bf16_down(dr) << 16);
+        }
+      }
+    } else if (__any(mm != 0u)) {  // wave-uniform: skip when no lane admits
 #pragma unroll
       for (int q = 0; q < 8; ++q) my_d2[64 * q] = make_float2(d[2 * q], d[2 * q + 1]);
       if (live && mm) {
@@ -551,8 +611,13 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) asm volatile("" ::"v"(qhi[kk]), "v"(qlo[kk]));
     asm volatile("" ::"v"(E2), "v"(na));
-    issue_stage(0, 0, 0);
-    issue_stage(min(1, nst - 1), 1, 1);
+    if constexpr (H3) {
+      issue_part3(0, 0, 0, 0);
+      issue_part3(0, 0, 0, 1);
+    } else {
+      issue_stage(0, 0, 0);
+      issue_stage(min(1, nst - 1), 1, 1);
+    }
     if (wid_u == 0) sNb[(NNB - 1) * kTT2 + lane] = INFINITY;
   } else {
     load_stage(0);
@@ -575,6 +640,50 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
       s_stamp[(wid * (kStampSt + 1) + kStampSt) * 4 + 3] = (uint64_t)p | ((uint64_t)nst << 32);
     }
   }
+  if constexpr (H3) {
+    // two buffers: stage st + 1 goes into stage st - 1's buffer (every wave is past it: the
+    // barrier), half of its pieces in each sub-tile region
+    for (int st = 0; st < nst; ++st) {
+      stage_barrier();
+      stamp(st, 0);
+      const int nbp = nbc == 0 ? NNB - 1 : nbc - 1, nbn = nbc == NNB - 1 ? 0 : nbc + 1;
+      const bool more = st + 1 < nst;
+      int vb[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) vb[kk] = frag[kk] + buf * BUFB;
+      {
+        float nb[16], d[16];
+        uint32_t mm = 0;
+        if (more) issue_part3(st + 1, buf ^ 1, nbn, 0);
+        load_nb(nbp, 1, nb);
+        mfma_sub(vb, 0, hA, xA);
+        epi(hB, xB, nb, d, mm);
+        interleave();
+        pin(b1, b2, mm);
+        append(mm, d, (st - 1) * kTT2 + 32);
+      }
+      stamp(st, 1);
+      {
+        float nb[16], d[16];
+        uint32_t mm = 0;
+        if (more) issue_part3(st + 1, buf ^ 1, nbn, 1);
+        load_nb(nbc, 0, nb);
+        mfma_sub(vb, 1, hB, xB);
+        epi(hA, xA, nb, d, mm);
+        interleave();
+        pin(b1, b2, mm);
+        append(mm, d, st * kTT2);
+      }
+      stamp(st, 2);
+      {
+        const float ob1 = other_half(b1), ob2 = other_half(b2);
+        thr_w = fminf(fminf(fmaxf(b1, ob1), fminf(b2, ob2)) + E2, thr_w);
+      }
+      stamp(st, 3);
+      nbc = nbn;
+      buf ^= 1;
+    }
+  } else {
   for (int st = 0; st < nst; ++st) {
     // stage st is visible, and every wave is done with stage st - 1 (DMA: st - 1's buffer
     // takes stage st + 2 at the end of this iteration; registers: stage st + 1): one barrier
@@ -630,6 +739,7 @@ __global__ void __launch_bounds__(kNT, 1) k_match_mfma(
     nbc = nbn;
     buf = buf == NBUF - 1 ? 0 : buf + 1;
   }
+  }  // !H3
   {
     uint32_t mm = 0;  // the last stage's sub-tile 1 (its norms: stage nst - 1)
     float nb[16], d[16];
@@ -1040,7 +1150,9 @@ __global__ void __launch_bounds__(256) k_match_overflow(const float* __restrict_
   }
 }
 
-size_t match_units_words(int P, int max_rows) { return 1 + (size_t)P * ((max_rows + kQB - 1) / kQB); }
+size_t match_units_words(int P, int max_rows) {  // for the smallest block (the half-CU form's)
+  return 1 + (size_t)P * ((max_rows + sweep_rows(3) - 1) / sweep_rows(3));
+}
 
 size_t match_pmax_bytes(int64_t capP) { return (size_t)(capP / kPrepRows) * sizeof(float2); }
 
@@ -1055,9 +1167,12 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
                        const void* pmax, const int32_t* pairs, int P, float ratio,
                        RowBest* rows, int max_rows, uint32_t* cand, int32_t* cand_n, float* cand_thr,
                        int* ovf_count, int2* ovf_list, int32_t* units, hipStream_t st) {
-  static const int stage = [] {  // SFMFEAT_MATCH_STAGE=reg: register-staged sweep (A/B timing)
+  // the half-CU form (STAGE 3) by default since round 5: 38.55k vs 37.91k img/s (six
+  // interleaved runs each, one box; 38.51k vs 37.90k over four on another);
+  // SFMFEAT_MATCH_STAGE=1 / reg: the one-workgroup-per-CU LDS-DMA / register-staged sweep (A/B)
+  static const int stage = [] {
     const char* e = getenv("SFMFEAT_MATCH_STAGE");
-    return (e && e[0] == 'r') ? 0 : 1;
+    return (e && e[0] == 'r') ? 0 : (e && e[0] == '1') ? 1 : 3;
   }();
   static const int rr8_max = [] {  // SFMFEAT_RERANK8_MAX: pair-count switch (A/B timing)
     const char* e = getenv("SFMFEAT_RERANK8_MAX");
@@ -1067,13 +1182,15 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
     const char* e = getenv("SFMFEAT_MATCH_UNITS");
     return !(e && e[0] == '0');
   }();
-  const int qb = (max_rows + kQB - 1) / kQB;
+  const int qbr = stage == 3 ? sweep_rows(3) : kQB;
+  const int qb = (max_rows + qbr - 1) / qbr;
   const dim3 grid((unsigned)(8 * ((P + 7) / 8) * qb));
   if (!use_units) units = nullptr;
-  if (units) hipLaunchKernelGGL(k_match_units, dim3(1), dim3(1024), 0, st, count, pairs, P, max_rows, units);
+  if (units) hipLaunchKernelGGL(k_match_units, dim3(1), dim3(1024), 0, st, count, pairs, P, max_rows, qbr, units);
   // ovf_count is zero here: set once at allocation, re-zeroed by k_match_compact
 #define SFM_SWEEP(A, ABL)                                                                             \
-  hipLaunchKernelGGL((k_match_mfma<A, ABL>), grid, dim3(kNT), 0, st, count, capP, hi, lo, norm2, rnorm,   \
+  hipLaunchKernelGGL((k_match_mfma<A, ABL>), grid, dim3(64 * sweep_waves(A)), 0, st, count, capP, hi, lo,  \
+                     norm2, rnorm,                                                                         \
                      static_cast<const float2*>(pmax), pairs, P, max_rows, cand, cand_n, cand_thr, ovf_count, \
                      ovf_list, units)
   static const int abl = [] {  // timing ablations: diagnostic build only (SFM_ABLATION_ENV)
@@ -1090,12 +1207,14 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
     case 16: SFM_SWEEP(1, 16); break;
     case 17: SFM_SWEEP(1, 17); break;
     case 32: SFM_SWEEP(1, 32); break;
-    default: if (stage == 0) SFM_SWEEP(0, 0); else SFM_SWEEP(1, 0);
+    default: if (stage == 0) SFM_SWEEP(0, 0); else if (stage == 3) SFM_SWEEP(3, 0); else SFM_SWEEP(1, 0);
   }
 #else
   (void)abl;
   if (stage == 0)
     SFM_SWEEP(0, 0);
+  else if (stage == 3)
+    SFM_SWEEP(3, 0);
   else
     SFM_SWEEP(1, 0);
 #endif

@@ -26,7 +26,8 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = {"1080p": (4, 1080, 1920, dict(P_OCT, num_interest_points=2500)),
          "4k": (2, 2160, 3840, dict(P_OCT, num_interest_points=8000, pyramid_level=5))}
-ALT_ENV = {"SFMFEAT_PYR_FUSED": "0", "SFMFEAT_RERANK2": "0", "SFMFEAT_EXACT_PX": "64", "SFMFEAT_SELECT_SUBSET": "0"}
+ALT_ENV = {"SFMFEAT_PYR_FUSED": "0", "SFMFEAT_RERANK2": "0", "SFMFEAT_EXACT_PX": "64", "SFMFEAT_SELECT_SUBSET": "0",
+           "SFMFEAT_MATCH_STAGE": "1"}
 
 
 def run_cases() -> dict:

@@ -1,17 +1,28 @@
 #!/bin/bash
-# A/B of environment switches on the headline bench: ab_env.sh "VAR=a" "VAR=b,VAR2=c" ... (each
-# run REPS times (2), interleaved; commas separate several variables of one variant); prints
-# img/s, ms/step and the per-stage ms of every run.
+# Same-box A/B/C... of one environment switch on the driver's bench: N rounds (default 4) of
+# `bench.py --steps 50 --warmup 5`, the values of VAR in turn each round (an empty value
+# leaves VAR unset).  usage: VAR=SFMFEAT_HARRIS_SLOTS VALS="448 512" bash tools/ab_env.sh [rounds]
+set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+N=${1:-4}
 mkdir -p gpurun_out
-for rep in $(seq 1 ${REPS:-2}); do
-  i=0
-  for e in "$@"; do
-    i=$((i+1))
-    env ${e//,/ } timeout -k 10 150 python bench.py --cpu-sample 0 ${BENCH_ARGS:-} > gpurun_out/ab_${i}_$rep.log 2>&1 || { tail -5 gpurun_out/ab_${i}_$rep.log; exit 1; }
-    tail -1 gpurun_out/ab_${i}_$rep.log | python -c '
-import json,sys
-d=json.loads(sys.stdin.read()); st=d.get("stages_ms",{})
-print(sys.argv[1], d["value"], d["ms_per_step"], "frac", (d.get("roofline") or {}).get("frac"), " ".join("%s=%s" % (k, v["ms_per_step"]) for k,v in st.items()))' "$e"
+: > gpurun_out/abe_runs.txt
+for i in $(seq 1 $N); do
+  for v in $VALS; do
+    if [ "$v" = "-" ]; then
+      timeout -k 10 200 env -u $VAR python bench.py --steps 50 --warmup 5 --cpu-sample 0 --no-profile > gpurun_out/abe.json 2> gpurun_out/abe.err || exit 1
+    else
+      env $VAR=$v timeout -k 10 200 python bench.py --steps 50 --warmup 5 --cpu-sample 0 --no-profile > gpurun_out/abe.json 2> gpurun_out/abe.err || exit 1
+    fi
+    python -c "import json;d=json.load(open('gpurun_out/abe.json'));print('$v', $i, d['value'], d['ms_per_step'])" | tee -a gpurun_out/abe_runs.txt
   done
 done
+python - <<'PY'
+import collections, statistics as st
+r = collections.defaultdict(list)
+for line in open("gpurun_out/abe_runs.txt"):
+    v, i, val, ms = line.split()
+    r[v].append(float(val))
+for v, xs in r.items():
+    print(f"{v}: mean {st.mean(xs):.0f} img/s, stdev {st.pstdev(xs):.0f}, n {len(xs)}")
+PY
