@@ -739,8 +739,10 @@ def run_gather(args, torch, dist, dev, rank, world):
       - the exchange is verified bit for bit once, after warm-up (per-frame checksums of
         what each owner sent vs. what every rank's table holds).
     strong scaling: n_global fixed (default 2048) for every N; weak: 256 frames per GPU.
-    Frames are device-resident uint8 (the u8 -> f32 conversion runs inside extraction),
-    tiled from up to 64 distinct synthetic frames per rank."""
+    Frames are device-resident float32 gray (u8 / 255, converted before timing as for the
+    configs[1] headline: until round 5 this job took u8 frames and timed the conversion,
+    ~80 us per 32-frame chunk, which configs[1] does not), tiled from up to 64 distinct
+    synthetic frames per rank."""
     from sfmfromscratch_amd import distributed as D
     from sfmfromscratch_amd import synth
 
@@ -752,8 +754,8 @@ def run_gather(args, torch, dist, dev, rank, world):
     S, C = plan.S, plan.C
     U = min(S, 64)
 
-    def frames_of(r, n):  # rank r's first n local frames, device-resident u8
-        uniq = np.stack([synth.make_frame_u8(H, W, 1234, r * S + i) for i in range(min(U, n))])
+    def frames_of(r, n):  # rank r's first n local frames, device-resident float32 gray
+        uniq = np.stack([synth.u8_to_gray(synth.make_frame_u8(H, W, 1234, r * S + i)) for i in range(min(U, n))])
         uq = torch.from_numpy(uniq).to(dev)
         return uq[torch.arange(n, device=dev) % uq.shape[0]].contiguous()
 
@@ -890,8 +892,8 @@ def run_gather(args, torch, dist, dev, rank, world):
             "value": round(n_global / tn, 2), "unit": "images/sec", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(tn * 1e3, 3),
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (deterministic integer-generated textured 1080p frames, device-resident uint8, "
-                    f"{U} distinct per rank, tiled)",
+            "data": "synthetic (deterministic integer-generated textured 1080p frames, device-resident float32 "
+                    f"gray (u8 / 255 before timing), {U} distinct per rank, tiled)",
             "config": {"workload": f"BASELINE configs[3]: {n_global}x 1080p sharded {S} per GPU, ScaleRotInvSIFT "
                                    "4-level x2 octave pyramid, k=2500, NNRatio 0.85, "
                                    + ("1-slot halo exchange" if job.halo else "chunked RCCL all-gather of the "
