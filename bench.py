@@ -164,6 +164,63 @@ def cpu_baseline(frames_per_thread: int):
     return n / dt, dt, nt, n
 
 
+def span_stats(spans, steps: int, flop: float, peak_tflops: float) -> dict:
+    """Roofline timing of the dominant kernel from its kernel-active spans (sfm_profile_spans:
+    per launch {earliest workgroup start, latest workgroup end} on the device's realtime clock;
+    `spans` holds one [n, 2] ns array per context, i.e. per lane, all on the same clock).
+
+    Two attributions of the kernel's time to the step, both over the timed region's launches:
+      - `union`: the measure of the union of all launches' intervals over every lane — the
+        time during which at least one launch of the kernel is active.  Non-overlapping:
+        two lanes' launches running at once count once, so it never exceeds the region;
+      - `launch_sum`: the sum of the launch durations (rocprofv3 --kernel-trace's per-launch
+        view): counts twice the time in which two lanes' launches overlap.
+    The roofline's `achieved` / `frac` use the union; the launch sum is reported beside it."""
+    iv = [np.asarray(s, dtype=np.int64).reshape(-1, 2) for s in spans]
+    iv = np.concatenate(iv) if iv else np.zeros((0, 2), np.int64)
+    iv = iv[(iv[:, 0] >= 0) & (iv[:, 1] >= iv[:, 0])]
+    n = int(len(iv))
+    if n == 0:
+        return {"launches": 0}
+    dur = (iv[:, 1] - iv[:, 0]).astype(np.float64)
+    order = np.argsort(iv[:, 0], kind="stable")
+    union, cur0, cur1 = 0, int(iv[order[0], 0]), int(iv[order[0], 1])
+    for k in order[1:]:
+        a, b = int(iv[k, 0]), int(iv[k, 1])
+        if a > cur1:
+            union += cur1 - cur0
+            cur0, cur1 = a, b
+        else:
+            cur1 = max(cur1, b)
+    union += cur1 - cur0
+    sum_ms, union_ms = float(dur.sum()) / 1e6, union / 1e6
+    return {"launches": n, "avg_launch_ms": round(sum_ms / n, 4),
+            "launch_sum_ms_per_step": round(sum_ms / steps, 4), "union_ms_per_step": round(union_ms / steps, 4),
+            "overlap_ms_per_step": round((sum_ms - union_ms) / steps, 4),
+            "first_to_last_ms": round((int(iv[:, 1].max()) - int(iv[:, 0].min())) / 1e6, 4),
+            "achieved_union": flop / 1e12 / (union_ms / 1e3), "achieved_launch_sum": flop / 1e12 / (sum_ms / 1e3),
+            "frac_union": flop / 1e12 / (union_ms / 1e3) / peak_tflops,
+            "frac_launch_sum": flop / 1e12 / (sum_ms / 1e3) / peak_tflops}
+
+
+def roofline_guard(roof: dict | None, ms_per_step: float, tol: float = 0.01) -> list:
+    """Consistency checks of a roofline entry against its own line (bench.py exits 4 when any
+    fails): the dominant kernel's attributed time per step must not exceed the step, and its
+    launch count must be positive.  `tol` absorbs the difference between the device's
+    realtime clock (spans) and the host / event clock of ms_per_step."""
+    bad = []
+    if not roof:
+        return bad
+    if not roof.get("launches"):
+        bad.append("roofline: no launches of the dominant kernel were timed")
+        return bad
+    att = roof.get("ms_per_step")
+    if att is None or att > ms_per_step * (1.0 + tol):
+        bad.append(f"roofline: {roof.get('kernel')} takes {att} ms per step by its own timing, more than the "
+                   f"{ms_per_step} ms step")
+    return bad
+
+
 def spin_until(ev):
     """Poll `ev` until the GPU has passed it, so the host sees the end of the timed work
     without a blocking wait's wake-up delay (measured up to ~3 ms on the box: a 20-step
@@ -207,10 +264,9 @@ def main():
     ap.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=8,
                     help="frames per host thread in the CPU baseline sample (0 = skip)")
-    ap.add_argument("--no-profile", action="store_true", help="disable the live per-stage HIP events")
-    ap.add_argument("--events-in-timed", action="store_true",
-                    help="A/B: bracket the dominant stage's launches with HIP events inside the timed region "
-                         "(default: a second, separate run of the same steps carries them)")
+    ap.add_argument("--no-profile", action="store_true", help="skip the untimed per-stage HIP-event pass (stages_ms)")
+    ap.add_argument("--no-spans", action="store_true",
+                    help="no kernel-active spans of the Harris launches in the timed region (no roofline)")
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default=None,
                     help="default: c2 at one GPU, c4 at N > 1.  "
                          "c2 = BASELINE configs[1] (the headline line); c3 = configs[2] (256 frames, all "
@@ -465,9 +521,13 @@ def main():
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     step_ev, host_ms = [], []
-    if dom and args.events_in_timed:  # A/B: the per-launch events inside the timed region
+    # the roofline's timing: kernel-active spans of every Harris launch inside the timed
+    # region itself (one atomic per workgroup; no events around the launches)
+    span_on = not args.no_spans
+    if span_on:
         for c in ctxs:
-            c.profile_stages([dom])
+            c.profile_spans(P_OCT["pyramid_level"] * (args.steps + 4))
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record()
     run_steps(args.steps, step_ev)
@@ -484,6 +544,18 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    spans = []
+    if span_on:
+        for c in ctxs:
+            sp, _, dropped = c.profile_spans_read()
+            if dropped:
+                raise SystemExit(f"bench.py: {dropped} Harris launches beyond the span capacity")
+            spans.append(sp)
+            c.profile_spans(0)
+    # the timed region's workload (keypoints per slot, matches per pair), before any later pass
+    # overwrites the lanes' tables
+    counts_l = lane_counts()
+    nmatch = np.concatenate([ln["mout"][2].cpu().numpy() for ln in pipe.lanes])
     # per-step end times inside the timed region (not part of `value`)
     step_end = [ev0.elapsed_time(e) for e in step_ev]
     step_detail = {"end_ms": [round(x, 4) for x in step_end],
@@ -510,21 +582,6 @@ def main():
                       "keypoints_per_level": [int(v) for v in lvl_kp],
                       "note": "modelled lane-ops per keypoint (bench.describe_ops) / 39.3 T lane-op/s"})
 
-    # the roofline: the same two-lane pipeline again, K steps, with HIP events around each
-    # launch of the dominant stage (kept out of the timed region above)
-    prof = {}
-    if dom and args.events_in_timed:
-        prof = prof_read()
-        prof_enable(False)
-    elif dom:
-        for c in ctxs:
-            c.profile_stages([dom])
-        prof_read()
-        torch.cuda.synchronize()
-        run_steps(args.steps)
-        torch.cuda.synchronize()
-        prof = prof_read()
-        prof_enable(False)
     # the same K steps again with one batch submitted every step (the pre-round-5 workload): the
     # line reports its rate beside `value` (alternating batches) as the cost of never re-reading
     # the previous step's frames
@@ -550,36 +607,40 @@ def main():
         same_value = world * B * args.steps / el
         same_batch[0] = False
 
-    counts_l = lane_counts()
-    counts = np.concatenate(counts_l) if len(counts_l) > 1 and batches is not None and len(batches) > 1 else counts_l[0]
-    nmatch = np.concatenate([ln["mout"][2].cpu().numpy() for ln in pipe.lanes])
-
     images = world * B * args.steps
     value = images / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
     roof = None
-    if dom:
-        # the dominant stage's launches inside the timed region, timed by their own events
+    if spans:
         traffic = {}
         # the committed PMC traffic was measured on the headline workload (c2) only
         if os.path.exists(TRAFFIC_FILE) and args.workload == "c2" and not args.rgb_ingest:
             with open(TRAFFIC_FILE) as f:
                 traffic = json.load(f).get("bytes_per_launch", {})
-        bound, amount, unit, peak, abytes = stage_work(counts_l, args.steps)[dom]
-        ms, n = prof[dom]
-        achieved = amount / (ms / 1e3)
-        kname = KERNELS[dom]
+        bound, amount, unit, peak, abytes = stage_work(counts_l, args.steps)["harris"]
+        st = span_stats(spans, args.steps, amount * 1e12, peak)
+        n = st["launches"]
+        kname = KERNELS["harris"]
         tr = traffic.get(kname)
-        alg_per_launch = abytes / max(n, 1) if abytes else None
-        roof = {"kernel": kname, "stage": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak,
-                "unit": unit, "frac": round(achieved / peak, 4), "traffic": tr,
+        alg_per_launch = abytes / max(n, 1) if abytes and n else None
+        roof = {"kernel": kname, "stage": "harris", "bound": bound,
+                "achieved": round(st["achieved_union"], 3) if n else None, "peak": peak, "unit": unit,
+                "frac": round(st["frac_union"], 4) if n else None, "traffic": tr,
                 "algorithmic_bytes_per_launch": round(alg_per_launch) if alg_per_launch else None,
                 "traffic_ratio": round(tr / alg_per_launch, 3) if tr and alg_per_launch else None,
-                "avg_launch_ms": round(ms / max(n, 1), 4), "launches": n,
-                "timing": (f"HIP events around each launch of the stage inside the timed region "
-                           f"({args.inflight} batches in flight)") if args.events_in_timed else
-                          (f"HIP events around each launch of the stage, on its stream, over a second run of the "
-                           f"timed region's {args.steps} steps ({args.inflight} batches in flight); the timed "
-                           f"region itself runs without per-launch events")}
+                "ms_per_step": st.get("union_ms_per_step"), "avg_launch_ms": st.get("avg_launch_ms"),
+                "launches": n,
+                "launch_sum": ({"ms_per_step": st["launch_sum_ms_per_step"],
+                                "achieved": round(st["achieved_launch_sum"], 3),
+                                "frac": round(st["frac_launch_sum"], 4),
+                                "overlap_ms_per_step": st["overlap_ms_per_step"],
+                                "note": "sum of the launch durations (rocprofv3 --kernel-trace's per-launch view): "
+                                        "counts twice the time two lanes' Harris launches overlap"} if n else None),
+                "dominant_stage_by_events": dom,
+                "timing": (f"kernel-active spans (sfm_profile_spans: earliest workgroup start to latest workgroup "
+                           f"end of each launch, device realtime clock) of every Harris launch inside the timed "
+                           f"region ({args.inflight} batches in flight); ms_per_step / achieved / frac = the "
+                           f"union of the launches' intervals over all lanes (non-overlapping attribution)")}
         if tr is not None:
             roof["traffic_note"] = "HBM bytes per launch, rocprofv3 PMC (profiles/pmc_traffic.json)"
 
@@ -600,7 +661,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -628,6 +689,10 @@ def main():
                                if same_value else None),
         }
         emit(out, args)
+        bad = roofline_guard(roof, ms_per_step)
+        if bad:
+            log("bench.py: " + "; ".join(bad))
+            sys.exit(4)
     if world > 1:
         dist.destroy_process_group()
 
@@ -841,29 +906,32 @@ def run_gather(args, torch, dist, dev, rank, world):
             comm = {"kind": f"halo: 1 slot point-to-point send/recv ({dist.get_backend()})",
                     "bytes_sent_per_rank": job.slot_bytes}
 
-    # timed region; Harris (the dominant kernel) bracketed by HIP events on rank 0's lanes
+    # timed region; Harris (the dominant kernel) timed by its kernel-active spans on rank 0's lanes
     ctxs = [ln["ex"].ctx for ln in job.lanes]
-    if not args.no_profile:
+    if not args.no_spans:
         for c in ctxs:
-            c.profile_enable(True)
-            c.profile_stages(["harris"])
-            c.profile_read(reset=True)
+            c.profile_spans(P_OCT["pyramid_level"] * C * (args.steps + 1))
     tn = timed(job, frames, args.steps)
     roof = None
-    if not args.no_profile:
-        ms = n = 0
+    if not args.no_spans:
+        spans = []
         for c in ctxs:
-            for k, (a, b) in c.profile_read(reset=True).items():
-                if k == "harris":
-                    ms, n = ms + a, n + b
-            c.profile_enable(False)
+            sp, _, dropped = c.profile_spans_read()
+            spans.append(sp)
+            c.profile_spans(0)
+            if dropped:
+                raise SystemExit(f"bench.py: {dropped} Harris launches beyond the span capacity")
         px = sum((H >> l) * (W >> l) for l in range(P_OCT["pyramid_level"])) * S * args.steps
-        if ms:
-            ach = HARRIS_FLOP_PER_PX * px / 1e12 / (ms / 1e3)
-            roof = {"kernel": KERNELS["harris"], "stage": "harris", "bound": "valu", "achieved": round(ach, 3),
-                    "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_TFLOPS, 4),
-                    "traffic": None, "avg_launch_ms": round(ms / max(n, 1), 4), "launches": n,
-                    "timing": "HIP events around each Harris launch of rank 0 inside the timed region"}
+        st = span_stats(spans, args.steps, HARRIS_FLOP_PER_PX * px, PEAK_F32_TFLOPS)
+        if st["launches"]:
+            roof = {"kernel": KERNELS["harris"], "stage": "harris", "bound": "valu",
+                    "achieved": round(st["achieved_union"], 3), "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(st["frac_union"], 4), "traffic": None, "ms_per_step": st["union_ms_per_step"],
+                    "avg_launch_ms": st["avg_launch_ms"], "launches": st["launches"],
+                    "launch_sum": {"ms_per_step": st["launch_sum_ms_per_step"],
+                                   "frac": round(st["frac_launch_sum"], 4)},
+                    "timing": "kernel-active spans of every Harris launch of this rank inside the timed region; "
+                              "frac from the union of their intervals over the lanes"}
 
     if args.verify:
         verify_gather_job(args, torch, dist, dev, job, frame_of, world, rank)
@@ -907,6 +975,10 @@ def run_gather(args, torch, dist, dev, rank, world):
             "collective": comm,
             "roofline": roof,
             "cpu_baseline": None}, args)
+        bad = roofline_guard(roof, tn * 1e3)
+        if bad:
+            log("bench.py: " + "; ".join(bad))
+            sys.exit(4)
     if world > 1:
         dist.destroy_process_group()
 

@@ -298,6 +298,19 @@ int32_t sfm_profile_enable(sfm_ctx* ctx, int32_t on);
  * bench times its headline run with the dominant stage's events alone. */
 int32_t sfm_profile_stages(sfm_ctx* ctx, int32_t mask);
 int32_t sfm_profile_read(sfm_ctx* ctx, double* ms, int64_t* launches, int32_t reset);
+/* Kernel-active spans of the Harris launches (the dominant kernel of the headline step):
+ * with capacity > 0, each of the context's next `capacity` Harris launches records
+ * {earliest workgroup start, latest workgroup end} on the device's constant-rate realtime
+ * clock (one atomic per workgroup, so it can stay on inside a timed region; unlike a pair of
+ * stream events it excludes the time a launch waits on its stream for CUs another stream
+ * holds).  capacity 0 turns it off.  Both calls reset the slots (and synchronise the device).
+ * sfm_profile_spans_read: spans_ns [n][2] in ns on that clock (comparable across the contexts
+ * of one device), levels [n] the first pyramid level of each launch, n_out the launches
+ * recorded (at most `capacity`), dropped the launches beyond it.
+ * (No reference counterpart: bench.py's roofline) */
+int32_t sfm_profile_spans(sfm_ctx* ctx, int64_t capacity);
+int32_t sfm_profile_spans_read(sfm_ctx* ctx, int64_t* spans_ns, int32_t* levels, int64_t cap, int64_t* n_out,
+                               int64_t* dropped, int32_t reset);
 
 /* ---------------- diagnostics (used by the parity tests) ----------------
  * Run individual stages of the same device code on host data. */

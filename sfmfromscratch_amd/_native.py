@@ -71,6 +71,8 @@ SIGNATURES = {
     "sfm_profile_enable": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "sfm_profile_stages": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "sfm_profile_read": (ctypes.c_int32, [_vp, ctypes.POINTER(ctypes.c_double), _i64p, ctypes.c_int32]),
+    "sfm_profile_spans": (ctypes.c_int32, [_vp, ctypes.c_int64]),
+    "sfm_profile_spans_read": (ctypes.c_int32, [_vp, _i64p, _i32p, ctypes.c_int64, _i64p, _i64p, ctypes.c_int32]),
     "sfm_debug_time_harris": (ctypes.c_float, [ctypes.c_int32] * 6),
     "sfm_debug_harris_stamps": (ctypes.c_float, [ctypes.c_int32] * 6 + [ctypes.c_void_p, ctypes.c_int64]),
     "sfm_debug_match_stamps": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int64]),
@@ -329,6 +331,22 @@ class Context:
         check(self.lib.sfm_profile_read(self.handle, ms.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
                                         n.ctypes.data_as(_i64p), 1 if reset else 0), self.handle)
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.PROF_STAGES)}
+
+    def profile_spans(self, capacity: int):
+        """Record the kernel-active span of each of the next `capacity` Harris launches (0: off)."""
+        check(self.lib.sfm_profile_spans(self.handle, int(capacity)), self.handle)
+
+    def profile_spans_read(self, reset: bool = True):
+        """-> (spans [n, 2] int64 ns on the device clock, first level [n], dropped launches)."""
+        n, dropped = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(self.lib.sfm_profile_spans_read(self.handle, None, None, 0, ctypes.byref(n), ctypes.byref(dropped), 0),
+              self.handle)
+        k = int(n.value)
+        sp = np.zeros((max(k, 1), 2), np.int64)
+        lv = np.zeros(max(k, 1), np.int32)
+        check(self.lib.sfm_profile_spans_read(self.handle, sp.ctypes.data_as(_i64p), lv.ctypes.data_as(_i32p), k,
+                                              ctypes.byref(n), ctypes.byref(dropped), 1 if reset else 0), self.handle)
+        return sp[:k], lv[:k], int(dropped.value)
 
     def match_pairs_dev(self, desc_ptr: int, count_ptr: int, nimg: int, cap: int, pairs_ptr: int, P: int,
                         ratio32: float, matches_ptr: int, conf_ptr: int, nmatch_ptr: int, stream: int = 0,

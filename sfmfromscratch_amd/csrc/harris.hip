@@ -221,6 +221,12 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
 
   const int tid = threadIdx.x;
   const int b = blockIdx.y;
+  // kernel-active span (bench.py's roofline timing; rocprofv3's kernel duration minus the
+  // dispatch latency): one atomic per workgroup at its start and at its exit
+  if (lvs.span != nullptr && tid == 0) atomicMin(lvs.span, (unsigned long long)wall_clock64());
+  auto span_end = [&]() {
+    if (lvs.span != nullptr && tid == 0) atomicMax(lvs.span + 1, (unsigned long long)wall_clock64());
+  };
   uint64_t* stamp = nullptr;
   int nst = 0;
   if constexpr (ABL == 3) {
@@ -712,7 +718,10 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     uint32_t c = s_hist[i] + (NHC == 2 ? s_hist[kHistCopy + i] : 0u);
     if (c) atomicAdd(&hg[i], c);
   }
-  if (scan.state == nullptr) return;
+  if (scan.state == nullptr) {
+    span_end();
+    return;
+  }
   // The last workgroup of this plane to finish runs the select scan.  The
   // flushes are device-scope atomics, performed at the memory side: waiting for their
   // acknowledgement (vmcnt) orders them before the arrival count without the L2
@@ -722,9 +731,13 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   __syncthreads();
   if (tid == 0) s_last = atomicAdd(&scan.done[(int64_t)b * kCounterStride], 1ull) == (unsigned long long)(nwg - 1) ? 1u : 0u;
   __syncthreads();
-  if (!s_last) return;
+  if (!s_last) {
+    span_end();
+    return;
+  }
   select_scan_plane(hg, scan.state + b, scan.list_count + (int64_t)b * kCounterStride, (int64_t)H * W,
                     scan.vmin, scan.force_exact, s_red);
+  span_end();
 }
 
 // Workgroups per plane for a group of levels: a common tile budget per workgroup

@@ -223,6 +223,10 @@ struct HarrisLevels {
   int n;
   int prio;  // 1: waves raise their issue priority with the tiles they have left (A/B)
   int stagger;  // n > 0: odd workgroups sleep n x 8k cycles before their first tile (A/B)
+  // kernel-active span of this launch (sfm_profile_spans; nullptr: off): {earliest workgroup
+  // start, latest workgroup end} on the device's constant-rate realtime clock, folded in with
+  // one atomic min / max per workgroup (the slot starts at {~0, 0})
+  unsigned long long* span;
 };
 void launch_harris_levels(const HarrisLevels& g, int B, const float* d_gauss, int ks, float alpha,
                           hipStream_t st);

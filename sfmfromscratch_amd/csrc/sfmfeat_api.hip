@@ -101,6 +101,11 @@ struct sfm_ctx {
   std::vector<hipEvent_t> prof_pool;
   double prof_ms[SFM_PROF_STAGES] = {0};
   int64_t prof_launches[SFM_PROF_STAGES] = {0};
+  // kernel-active spans of the Harris launches (sfm_profile_spans): span_cap slots of
+  // {start, end} realtime ticks, the next free slot, each slot's first pyramid level
+  DevBuf d_spans;
+  int64_t span_cap = 0, span_n = 0, span_dropped = 0;
+  std::vector<int32_t> span_level;
 };
 
 namespace {
@@ -470,6 +475,14 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
           q.down[2] = const_cast<float*>(lvl[3]);
         }
       }
+      if (c->span_cap > 0) {
+        if (c->span_n < c->span_cap) {
+          g.span = as<unsigned long long>(c->d_spans) + 2 * c->span_n++;
+          c->span_level.push_back(l0);
+        } else {
+          ++c->span_dropped;
+        }
+      }
       if (!(l0 > 0 && (skip & 16))) launch_harris_levels(g, B, as<float>(c->d_gauss), c->p.gaussian_size, alpha, st);
     }
     if (pyr_fused && l0 == 0 && L > 4) {
@@ -764,7 +777,7 @@ int32_t sfm_ctx_destroy(sfm_ctx* c) {
                     &c->m_hi, &c->m_lo, &c->m_norm2, &c->m_rnorm, &c->m_imgmax, &c->m_ovf, &c->m_ovfc, &c->m_cand, &c->m_candn, &c->m_candt, &c->m_units,
                     &c->i_tab_h, &c->i_tab_v, &c->i_tmp, &c->i_rgb, &c->i_gray, &c->i_colmap, &c->i_sets,
                     &c->r_idx, &c->r_off, &c->r_F, &c->r_counts, &c->r_pts, &c->r_npts, &c->r_out, &c->r_on,
-                    &c->r_oit};
+                    &c->r_oit, &c->d_spans};
   for (DevBuf* b : bufs) free_buf(*b);
   for (auto& e : c->prof_pending) {
     (void)hipEventDestroy(e.second.first);
@@ -1239,6 +1252,55 @@ int32_t sfm_profile_read(sfm_ctx* c, double* ms, int64_t* launches, int32_t rese
     }
   }
   return SFM_OK;
+}
+
+namespace {
+// every span slot back to {~0, 0} (the kernels fold their workgroups in with atomic min / max)
+int spans_reset(sfm_ctx* c) {
+  c->span_n = 0;
+  c->span_dropped = 0;
+  c->span_level.clear();
+  if (c->span_cap == 0) return SFM_OK;
+  std::vector<unsigned long long> init((size_t)2 * c->span_cap, 0ull);
+  for (int64_t i = 0; i < c->span_cap; ++i) init[2 * i] = ~0ull;
+  HIPCHK(c, hipDeviceSynchronize());
+  HIPCHK(c, hipMemcpy(c->d_spans.p, init.data(), init.size() * 8, hipMemcpyHostToDevice));
+  return SFM_OK;
+}
+}  // namespace
+
+int32_t sfm_profile_spans(sfm_ctx* c, int64_t capacity) {
+  if (!c || capacity < 0) return SFM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if (capacity > 0 && (rc = ensure(c, c->d_spans, (size_t)capacity * 16))) return rc;
+  c->span_cap = capacity;
+  return spans_reset(c);
+}
+
+int32_t sfm_profile_spans_read(sfm_ctx* c, int64_t* spans_ns, int32_t* levels, int64_t cap, int64_t* n_out,
+                               int64_t* dropped, int32_t reset) {
+  if (!c || !n_out || cap < 0) return SFM_EINVAL;
+  HIPCHK(c, hipSetDevice(c->device));
+  *n_out = c->span_n;
+  if (dropped) *dropped = c->span_dropped;
+  if (c->span_n > 0 && spans_ns && cap > 0) {
+    int khz = 0;
+    HIPCHK(c, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+    if (khz <= 0) return set_err(c, SFM_EDEVICE, "device reports no wall-clock rate");
+    HIPCHK(c, hipDeviceSynchronize());
+    const int64_t n = std::min(cap, c->span_n);
+    std::vector<unsigned long long> h((size_t)2 * n);
+    HIPCHK(c, hipMemcpy(h.data(), c->d_spans.p, h.size() * 8, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; ++i) {
+      for (int k = 0; k < 2; ++k) {  // ticks -> ns; an untouched slot reads -1
+        const unsigned long long t = h[2 * i + k];
+        spans_ns[2 * i + k] = (t == ~0ull || (k == 1 && t == 0ull)) ? -1 : (int64_t)((long double)t * 1.0e6L / khz);
+      }
+      if (levels) levels[i] = c->span_level[(size_t)i];
+    }
+  }
+  return reset ? spans_reset(c) : SFM_OK;
 }
 
 int32_t sfm_match_pairs_dev(sfm_ctx* c, const float* desc, const int32_t* count, int32_t nimg,

@@ -80,3 +80,37 @@ def test_shipped_library_has_no_ablations():
     for name in (b"SFMFEAT_SKIP", b"SFMFEAT_HARRIS_ABL", b"SFMFEAT_SELECT_ABL", b"SFMFEAT_DQ_ABL", b"SFMFEAT_MATCH_ABL",
                  b"SFMFEAT_NMS_DRY"):
         assert name not in data, name
+
+
+def test_span_stats_union_and_launch_sum():
+    """The roofline's timing from kernel-active spans: two lanes' launches that overlap count
+    once in the union (non-overlapping attribution) and twice in the launch sum."""
+    sys.path.insert(0, ROOT)
+    import numpy as np
+
+    import bench
+    ms = 1_000_000  # ns
+    lane_a = np.array([[0, 4 * ms], [10 * ms, 12 * ms]], np.int64)
+    lane_b = np.array([[3 * ms, 6 * ms], [20 * ms, 21 * ms], [-1, -1]], np.int64)  # an unused slot is dropped
+    st = bench.span_stats([lane_a, lane_b], steps=2, flop=2e12, peak_tflops=100.0)
+    assert st["launches"] == 4
+    assert st["launch_sum_ms_per_step"] == 5.0          # (4 + 2 + 3 + 1) / 2
+    assert st["union_ms_per_step"] == 4.5              # ([0, 6] + [10, 12] + [20, 21]) / 2
+    assert st["overlap_ms_per_step"] == 0.5
+    assert st["first_to_last_ms"] == 21.0
+    assert abs(st["achieved_union"] - 2.0 / 9e-3) < 1e-6   # 2 TFLOP over 9 ms
+    assert abs(st["frac_launch_sum"] - 2.0 / 10e-3 / 100.0) < 1e-9
+    assert bench.span_stats([np.zeros((0, 2), np.int64)], 1, 1.0, 1.0) == {"launches": 0}
+
+
+def test_roofline_guard_rejects_more_kernel_time_than_the_step():
+    """bench.py exits 4 when the dominant kernel's attributed time per step exceeds the step
+    (the round-5 line implied 0.948 ms of Harris per 0.812 ms step) or nothing was timed."""
+    sys.path.insert(0, ROOT)
+    import bench
+    ok = {"kernel": "k_harris<7>", "launches": 80, "ms_per_step": 0.70}
+    assert bench.roofline_guard(ok, 0.812) == []
+    assert bench.roofline_guard(None, 0.812) == []
+    assert bench.roofline_guard(dict(ok, ms_per_step=0.948), 0.812)
+    assert bench.roofline_guard(dict(ok, ms_per_step=0.815), 0.812) == []   # within the clock tolerance
+    assert bench.roofline_guard(dict(ok, launches=0), 0.812)
