@@ -21,6 +21,11 @@
 #else
 #define SFM_ABLATION_ENV(name) ((const char*)nullptr)
 #endif
+// Diagnostic A/B switches (alternative layouts, launch shapes and stream schedules that were
+// measured slower and are kept for experiments): like the ablations, read only by the
+// diagnostic build.  The shipped library reads only the product switches, each of which
+// tests/test_gpu_switches.py runs against the default bit for bit (PRODUCT_SWITCHES there).
+#define SFM_DIAG_ENV(name) SFM_ABLATION_ENV(name)
 
 namespace sfm {
 

@@ -758,8 +758,12 @@ static int harris_plan(HarrisLevels& g, int B, int slots) {
   return wg;
 }
 
-static int env_int(const char* name, int dflt) {
+static int env_int(const char* name, int dflt) {  // product switch (tests/test_gpu_switches.py)
   const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+static int diag_int(const char* name, int dflt) {  // diagnostic build only (SFM_DIAG_ENV)
+  const char* e = SFM_DIAG_ENV(name);
   return e ? atoi(e) : dflt;
 }
 
@@ -775,7 +779,7 @@ static void launch_form(HarrisLevels g, int B, const float* gk, float alpha, hip
   static const int slots_env = env_int("SFMFEAT_HARRIS_SLOTS", 0);
   // SFMFEAT_HARRIS_SLOTS_UPPER=n (A/B): the budget of levels above the first (fewer than
   // 200 64 x 64 tiles per plane)
-  static const int slots_up = env_int("SFMFEAT_HARRIS_SLOTS_UPPER", 0);
+  static const int slots_up = diag_int("SFMFEAT_HARRIS_SLOTS_UPPER", 0);
   int slots2 = slots_env > 0 ? slots_env : (B >= 16 ? 448 : 480);
   if (slots_up > 0 && g.n == 1 && ((g.l[0].W + kHT - 1) / kHT) * ((g.l[0].H + kHT - 1) / kHT) < 200) slots2 = slots_up;
   bool vec = true;
@@ -794,39 +798,47 @@ static void launch_form(HarrisLevels g, int B, const float* gk, float alpha, hip
 template <int KS, int ABL = 0>
 static void launch_ks(HarrisLevels g, int B, const float* gk, float alpha, hipStream_t st) {
   // SFMFEAT_HARRIS_PRIO=1: tile-balancing issue priority (A/B)
-  static const int prio = env_int("SFMFEAT_HARRIS_PRIO", 0);
+  static const int prio = diag_int("SFMFEAT_HARRIS_PRIO", 0);
   // SFMFEAT_HARRIS_NPAIR=1: the four-wave form for every level (A/B)
-  static const int npair = env_int("SFMFEAT_HARRIS_NPAIR", 2);
+  static const int npair = diag_int("SFMFEAT_HARRIS_NPAIR", 2);
   // SFMFEAT_HARRIS_SMALL=t: levels whose 64 x 64 tiles number at most t per resident
   // workgroup (over the batch) take the 64 x 32 form (0: never)
-  static const int small = env_int("SFMFEAT_HARRIS_SMALL", kHarrisSmallTiles);
+  static const int small = diag_int("SFMFEAT_HARRIS_SMALL", kHarrisSmallTiles);
   g.prio = prio;
   // SFMFEAT_HARRIS_STAGGER=n: odd workgroups sleep n x 8k cycles before their first tile (A/B)
-  static const int stagger = env_int("SFMFEAT_HARRIS_STAGGER", 0);
+  static const int stagger = diag_int("SFMFEAT_HARRIS_STAGGER", 0);
   g.stagger = stagger;
   // SFMFEAT_HARRIS_PP=1: product planes in LDS (form 3) instead of gradient planes (A/B)
-  static const int pp = env_int("SFMFEAT_HARRIS_PP", kHarrisProductPlanes);
+  static const int pp = diag_int("SFMFEAT_HARRIS_PP", kHarrisProductPlanes);
   // SFMFEAT_HARRIS_MF=1: window sums on the matrix pipe (form 4) for the levels that take
   // form 0; 2: for every level; 3 / 4: S_xy on MFMA beside the VALU (form 5), form-0 levels
   // / every level
-  static const int mf = env_int("SFMFEAT_HARRIS_MF", kHarrisMfma);
+  static const int mf = diag_int("SFMFEAT_HARRIS_MF", kHarrisMfma);
   if constexpr (KS == 7) {  // the alternative forms are built for the 7 x 7 window only
     // the fused pyramid (levels with down[0] set) is validated in form 0 only
     bool fused = false;
     for (int k = 0; k < g.n; ++k) fused = fused || g.l[k].down[0] != nullptr;
     if (fused) return launch_form<KS, ABL, 0>(g, B, gk, alpha, st);
+#ifdef SFM_ABLATIONS  // the forms measured slower (1, 3, 4, 5): diagnostic build only
     if (npair == 1) return launch_form<KS, ABL, 1>(g, B, gk, alpha, st);
     if (mf == 2) return launch_form<KS, ABL, 4>(g, B, gk, alpha, st);
     if (mf == 4) return launch_form<KS, ABL, 5>(g, B, gk, alpha, st);
+#else
+    (void)npair;
+    (void)pp;
+    (void)mf;
+#endif
     bool sm = small > 0;
     for (int k = 0; k < g.n; ++k) {
       const int64_t t64 = (int64_t)((g.l[k].W + kHT - 1) / kHT) * ((g.l[k].H + kHT - 1) / kHT) * B;
       sm = sm && t64 <= (int64_t)small * 512;
     }
     if (sm) return launch_form<KS, ABL, 2>(g, B, gk, alpha, st);
+#ifdef SFM_ABLATIONS
     if (pp == 1) return launch_form<KS, ABL, 3>(g, B, gk, alpha, st);
     if (mf == 1) return launch_form<KS, ABL, 4>(g, B, gk, alpha, st);
     if (mf == 3) return launch_form<KS, ABL, 5>(g, B, gk, alpha, st);
+#endif
   }
   launch_form<KS, ABL, 0>(g, B, gk, alpha, st);
 }

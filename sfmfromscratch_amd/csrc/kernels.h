@@ -24,6 +24,9 @@ constexpr int kTopkLdsCap = 8192;           // max keys sorted in LDS by the top
 constexpr int kMaxMatchRows = 16384;        // max keypoints per image for the matcher sort
 constexpr int kMatchCandCap = 256;          // admitted targets per query row (MFMA matcher lists)
 constexpr int kCounterStride = 32;          // u64 per per-plane atomic counter (own 256-B line)
+// the sweep's work units (k_match_units) encode pair | block << kMatchUnitPairBits: one
+// matcher sub-launch takes at most 2^kMatchUnitPairBits pairs (match_impl clamps)
+constexpr int kMatchUnitPairBits = 20;
 
 // Per-plane state of the keypoint selection (NaiveSIFT.py:90-120).
 //

@@ -176,7 +176,10 @@ static_assert(kSweepLds <= 160 * 1024, "LDS per CU");
 // and Harris's VALU then share the SIMDs instead of taking CUs in turn
 constexpr int kWaves3 = 4;
 constexpr size_t kSweepLds3 = (size_t)2 * 2 * kTT2 * 256 + 3 * kTT2 * 4 + 256;
-static_assert(kSweepLds3 + 80 * 1024 <= 160 * 1024, "half-CU sweep beside one Harris workgroup");
+// (the Harris side is checked on the built code objects: tests/test_isa_guard_cpu.py
+// test_half_cu_sweep_fits_beside_one_harris_workgroup reads both kernels' LDS from the
+// metadata; this bound only keeps the sweep within half of the CU's LDS)
+static_assert(kSweepLds3 <= 80 * 1024, "half-CU sweep: at most half of the CU's LDS");
 constexpr int sweep_waves(int stage) { return stage == 3 ? kWaves3 : kWaves; }
 constexpr int sweep_rows(int stage) { return kQW * sweep_waves(stage); }
 
@@ -256,7 +259,7 @@ __global__ void __launch_bounds__(1024) k_match_units(const int32_t* __restrict_
       tot += t;
     }
     const uint32_t first = base + before + x - q;
-    for (uint32_t j = 0; j < q; ++j) units[1 + first + j] = (int32_t)((uint32_t)p | (j << 20));
+    for (uint32_t j = 0; j < q; ++j) units[1 + first + j] = (int32_t)((uint32_t)p | (j << kMatchUnitPairBits));
     base += tot;
     __syncthreads();
   }
@@ -323,8 +326,8 @@ __global__ void __launch_bounds__(64 * sweep_waves(STAGE), STAGE == 3 ? 2 : 1) k
     const int u = grp * cu + slot8;
     if (slot8 >= cu || u >= U) return;
     const int code = units[1 + u];
-    p = code & 0xFFFFF;
-    row0 = (code >> 20) * QBR;
+    p = code & ((1 << kMatchUnitPairBits) - 1);
+    row0 = (code >> kMatchUnitPairBits) * QBR;
   } else {  // SFMFEAT_MATCH_UNITS=0: pairs p = grp (mod 8) on XCD grp, every block slot (A/B)
     p = grp + 8 * (slot8 / QB);
     row0 = (slot8 % QB) * QBR;
@@ -1175,11 +1178,11 @@ void launch_match_mfma(const float* desc, const int32_t* count, int64_t cap, int
     return (e && e[0] == 'r') ? 0 : (e && e[0] == '1') ? 1 : 3;
   }();
   static const int rr8_max = [] {  // SFMFEAT_RERANK8_MAX: pair-count switch (A/B timing)
-    const char* e = getenv("SFMFEAT_RERANK8_MAX");
+    const char* e = SFM_DIAG_ENV("SFMFEAT_RERANK8_MAX");
     return e ? atoi(e) : kRerank8MaxPairs;
   }();
   static const bool use_units = [] {  // SFMFEAT_MATCH_UNITS=0: the per-pair XCD mapping (A/B)
-    const char* e = getenv("SFMFEAT_MATCH_UNITS");
+    const char* e = SFM_DIAG_ENV("SFMFEAT_MATCH_UNITS");
     return !(e && e[0] == '0');
   }();
   const int qbr = stage == 3 ? sweep_rows(3) : kQB;

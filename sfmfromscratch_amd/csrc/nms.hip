@@ -526,9 +526,9 @@ static void launch_tile(const float* R, const MedianState* state, uint64_t* cand
   if (KH == 1 && mode == 0 && vec && !force_tile && !nms_tile_forced()) {
     // SFMFEAT_NMS_SH=8: 8-row strips (A/B); SFMFEAT_NMS_DRY=1: a candidate-free read pass
     // of R ahead of the real one (timing only: how fast R reads once Harris's writes drained)
-    static const int sh = [] { const char* e = getenv("SFMFEAT_NMS_SH"); return e ? atoi(e) : kStreamSH; }();
+    static const int sh = [] { const char* e = SFM_DIAG_ENV("SFMFEAT_NMS_SH"); return e ? atoi(e) : kStreamSH; }();
     static const bool dry = [] { const char* e = SFM_ABLATION_ENV("SFMFEAT_NMS_DRY"); return e && atoi(e) != 0; }();
-    static const int band = [] { const char* e = getenv("SFMFEAT_NMS_BAND"); return e ? atoi(e) : kBandStrips; }();
+    static const int band = [] { const char* e = SFM_DIAG_ENV("SFMFEAT_NMS_BAND"); return e ? atoi(e) : kBandStrips; }();
     if (band >= 1 && band <= 4 && !dry) {
       const int rows = 8 * band;
       const int nbands = (H + rows - 1) / rows;
@@ -546,7 +546,7 @@ static void launch_tile(const float* R, const MedianState* state, uint64_t* cand
     const int NTr = 256;
     const int nstrips = (H + SHr - 1) / SHr;
     const int64_t threads = (int64_t)(W >> 2) * nstrips;
-    static const int wg = [] { const char* e = getenv("SFMFEAT_NMS_STREAM_WG"); return e ? atoi(e) : 0; }();
+    static const int wg = [] { const char* e = SFM_DIAG_ENV("SFMFEAT_NMS_STREAM_WG"); return e ? atoi(e) : 0; }();
     const int64_t nvb = (threads + NTr - 1) / NTr;
     // SFMFEAT_NMS_STREAM_WG=n: at most n workgroups per launch over all planes (persistent)
     dim3 grid((unsigned)(wg > 0 ? std::min<int64_t>(nvb, std::max(1, wg / std::max(B, 1))) : nvb), B);
@@ -563,7 +563,7 @@ static void launch_tile(const float* R, const MedianState* state, uint64_t* cand
   // contiguous row-major tile ranges per workgroup (enough workgroups to keep the bytes in
   // flight: each holds one tile of prefetch)
   static const int slots = [] {  // SFMFEAT_NMS_SLOTS: workgroups per launch over all planes (A/B)
-    const char* e = getenv("SFMFEAT_NMS_SLOTS");
+    const char* e = SFM_DIAG_ENV("SFMFEAT_NMS_SLOTS");
     return e ? atoi(e) : 0;
   }();
   const int per_plane = slots > 0 ? std::max(1, slots / std::max(B, 1)) : kNmsBlocksPerPlane;

@@ -230,7 +230,8 @@ SFM_DEV int lds_wave_append(uint32_t* counter, bool pred) {
 SFM_DEV bool topk_subset(const uint64_t* cp, int64_t C, int kk, const uint32_t (&tsub)[2], uint32_t tnms,
                          const SelectLds& L) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  if (C <= kTopkDirect || C > (int64_t)kRegKeys * nt || tsub[1] <= tnms) return false;
+  // (tsub[0] >= tsub[1] >= tnms: when tsub[0] == tnms both subsets are the whole list)
+  if (C <= kTopkDirect || C > (int64_t)kRegKeys * nt || tsub[0] <= tnms) return false;
   uint64_t kr[kRegKeys];
 #pragma unroll
   for (int j = 0; j < kRegKeys; ++j) {
@@ -255,7 +256,7 @@ SFM_DEV bool topk_subset(const uint64_t* cp, int64_t C, int kk, const uint32_t (
   __syncthreads();
   const uint32_t n0 = L.cnt[0], n1 = L.cnt[1];
   const int t = (n0 >= (uint32_t)kk && n0 <= (uint32_t)kTopkDirect) ? 0
-              : (n1 >= (uint32_t)kk && n1 <= (uint32_t)kTopkDirect) ? 1 : -1;
+              : (tsub[1] > tnms && n1 >= (uint32_t)kk && n1 <= (uint32_t)kTopkDirect) ? 1 : -1;
   if (t < 0) return false;  // (uniform)
   const uint32_t ht = t == 0 ? h0 : h1;
   __syncthreads();

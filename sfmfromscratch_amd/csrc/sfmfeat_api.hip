@@ -301,7 +301,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   // the first three-level pyramid pass also zeroes the histograms and append counters
   const size_t hist_bytes = (size_t)L * B * kMedBins1 * 4, count_bytes = (size_t)4 * L * B * 8 * kCounterStride;
   static const bool fill_launches = [] {  // SFMFEAT_FILL_LAUNCHES=1: separate fills (A/B)
-    const char* e = getenv("SFMFEAT_FILL_LAUNCHES");
+    const char* e = SFM_DIAG_ENV("SFMFEAT_FILL_LAUNCHES");
     return e && atoi(e) != 0;
   }();
   bool zeroed = fill_launches;
@@ -433,14 +433,14 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   // share launches (up to kHarrisMaxLevels each).  Off by default: grouping L1-L3 or L2-L3 cut
   // the Harris stage time by ~2% but the pipeline lost more overlap than that (DESIGN_LOG.md §B).
   static const int group_from = [] {
-    const char* e = getenv("SFMFEAT_HARRIS_GROUP");
+    const char* e = SFM_DIAG_ENV("SFMFEAT_HARRIS_GROUP");
     return e ? atoi(e) : 0;
   }();
   // the lane gate's release point: after the Harris launch of level gate_level (default 0:
   // the next gated extraction's pyramid and level-0 Harris follow this one's level-0 Harris;
   // SFMFEAT_GATE_LEVEL=-1: after every level's Harris and NMS)
   static const int gate_level = [] {
-    const char* e = getenv("SFMFEAT_GATE_LEVEL");
+    const char* e = SFM_DIAG_ENV("SFMFEAT_GATE_LEVEL");
     return e ? atoi(e) : 0;
   }();
   bool gate_released = false;
@@ -500,7 +500,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
         // SFMFEAT_SELECT_CALLER=1 (A/B): the level's selection on the caller's stream ahead of
         // the next level's Harris, only its descriptors on aux
         static const bool sel_caller = [] {
-          const char* e = getenv("SFMFEAT_SELECT_CALLER");
+          const char* e = SFM_DIAG_ENV("SFMFEAT_SELECT_CALLER");
           return e && atoi(e) == 1;
         }();
         if (sel_caller) select_level(l, st);
@@ -517,7 +517,7 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   // the caller stream's levels: one selection launch for all of them (each level its own
   // scratch regions inside the stream's half), unless SFMFEAT_SELECT_MERGE=0
   static const bool merge_select = [] {
-    const char* e = getenv("SFMFEAT_SELECT_MERGE");
+    const char* e = SFM_DIAG_ENV("SFMFEAT_SELECT_MERGE");
     return !(e && atoi(e) == 0);
   }();
   if (merge_select && L - L_aux > 1 && L - L_aux <= kSelectMaxLevels) {
@@ -606,7 +606,10 @@ int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, in
   // allocation that grows with P * cap.
   const size_t budget = c->match_budget;
   const size_t per_pair = (size_t)cap * (sizeof(RowBest) + sizeof(int2) + (c->match_direct ? 0 : kMatchCandCap * 4 + 8));
-  const int Pmax = (int)std::max<size_t>(1, std::min<size_t>((size_t)P, budget / per_pair));
+  // (at most 2^kMatchUnitPairBits pairs per sub-launch: the sweep's work units hold the pair
+  // index in that many bits, so a small capacity under a large budget cannot wrap it)
+  const int Pmax = (int)std::max<size_t>(
+      1, std::min<size_t>(std::min<size_t>((size_t)P, budget / per_pair), (size_t)1 << kMatchUnitPairBits));
   if ((rc = ensure(c, c->m_rows, (size_t)Pmax * cap * sizeof(RowBest)))) return rc;
   if ((rc = ensure(c, c->m_ovf, (size_t)Pmax * cap * sizeof(int2)))) return rc;
   if (c->m_ovfc.bytes == 0) {  // the overflow counter starts at zero; k_match_compact re-zeroes it
@@ -736,7 +739,7 @@ int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out) {
   // the caller's stream layout under the caller's control (pipeline.BatchPipeline).
   bool ok = hipSetDevice(device) == hipSuccess;
   {  // SFMFEAT_EAGER_HOST_STREAM=1 (A/B): the round-3 stream layout (both made here)
-    const char* e = getenv("SFMFEAT_EAGER_HOST_STREAM");
+    const char* e = SFM_DIAG_ENV("SFMFEAT_EAGER_HOST_STREAM");
     if (ok && e && atoi(e) == 1)
       ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
            hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess;

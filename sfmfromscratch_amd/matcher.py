@@ -51,9 +51,9 @@ class NNRatioFeatureMatcher:
             raise IndexError("index 1 is out of bounds for axis 0 with size %d" % n2)
         if n1 == 0:
             return np.array([]), np.array([])
-        from .sift import _DEVICE
+        from .sift import current_device
         params = _abi.params_from_dict({}, _abi.SFM_MODE_NAIVE)
-        m, c = context_for(params, _DEVICE).match(f1.reshape(n1, 128), f2.reshape(n2, 128),
+        m, c = context_for(params, current_device()).match(f1.reshape(n1, 128), f2.reshape(n2, 128),
                                                   ratio_as_float32(self.ratio_threshold))
         if len(c) == 0:
             return np.array([]), np.array([])

@@ -8,6 +8,7 @@ no CPU fallback: without the library or a GPU, construction / detection raises.
 from __future__ import annotations
 
 import os
+import threading
 from typing import Tuple
 
 import numpy as np
@@ -16,13 +17,20 @@ from . import _abi
 from ._native import context_for
 from .feature_extractor import FeatureExtractor
 
-_DEVICE = int(os.environ.get("SFMFEAT_DEVICE", "0"))
+_DEFAULT_DEVICE = int(os.environ.get("SFMFEAT_DEVICE", "0"))
+_tls = threading.local()
 
 
 def set_device(device: int) -> None:
-    """HIP device used by the drop-in classes of this thread's future calls."""
-    global _DEVICE
-    _DEVICE = int(device)
+    """HIP device used by the drop-in classes (extractors and matcher) for this thread's
+    future calls; other threads keep theirs (the reference drives the classes from 8 threads,
+    Runner.py:183-191).  A thread that never calls it uses SFMFEAT_DEVICE (default 0)."""
+    _tls.device = int(device)
+
+
+def current_device() -> int:
+    """This thread's device for the drop-in classes (set_device, else SFMFEAT_DEVICE)."""
+    return getattr(_tls, "device", _DEFAULT_DEVICE)
 
 
 def _reference_fvs(desc: np.ndarray) -> np.ndarray:
@@ -51,7 +59,7 @@ class NaiveSIFT(FeatureExtractor):
         img = np.asarray(self.image)
         assert img.ndim == 2, "Image must be grayscale"
         params = _abi.params_from_dict(self._extractor_params, mode)
-        return context_for(params, _DEVICE).extract(img)
+        return context_for(params, current_device()).extract(img)
 
     def detect_keypoints(self) -> Tuple[np.ndarray, np.ndarray]:
         """Detect interest points using Harris corner detection (NaiveSIFT.py:42-45)."""
@@ -107,4 +115,4 @@ class ScaleRotInvSIFT(NaiveSIFT):
         img = np.asarray(self.image)
         assert img.ndim == 2, "Image must be grayscale"
         p = _abi.params_from_dict(params, _abi.SFM_MODE_SCALEROT)
-        return context_for(p, _DEVICE).extract(img)
+        return context_for(p, current_device()).extract(img)

@@ -129,3 +129,30 @@ def test_resize_dims_like_runner():
         assert resize_dims(H, W, s) == (int(H * s), int(W * s))
     with pytest.raises(ValueError):
         resize_dims(1, 1, 0.5)
+
+
+def test_set_device_is_thread_local():
+    """set_device (the drop-in classes' device) belongs to the calling thread: the reference
+    drives the classes from 8 threads (Runner.py:183-191), so one thread's choice must not move
+    another's work.  No device call is made."""
+    import threading
+
+    from sfmfromscratch_amd import set_device
+    from sfmfromscratch_amd.sift import current_device
+    base = current_device()
+    seen = {}
+
+    def other():
+        seen["before"] = current_device()
+        set_device(5)
+        seen["after"] = current_device()
+
+    set_device(3)
+    try:
+        th = threading.Thread(target=other)
+        th.start()
+        th.join()
+        assert seen == {"before": base, "after": 5}
+        assert current_device() == 3
+    finally:
+        set_device(base)

@@ -114,3 +114,22 @@ def test_roofline_guard_rejects_more_kernel_time_than_the_step():
     assert bench.roofline_guard(dict(ok, ms_per_step=0.948), 0.812)
     assert bench.roofline_guard(dict(ok, ms_per_step=0.815), 0.812) == []   # within the clock tolerance
     assert bench.roofline_guard(dict(ok, launches=0), 0.812)
+
+
+def test_shipped_library_reads_only_product_switches():
+    """Every SFMFEAT_* name in the shipped library is a product switch that
+    tests/test_gpu_switches.py runs against the default bit for bit; the diagnostic A/B
+    switches (slower Harris forms, NMS strip shapes, stream-schedule experiments) exist only
+    in the diagnostic build (SFM_DIAG_ENV)."""
+    import re
+    sys.path.insert(0, ROOT)
+    from tests.test_gpu_switches import PRODUCT_SWITCHES
+    lib = os.path.join(ROOT, "sfmfromscratch_amd", "lib", "libsfmfeat.so")
+    if not os.path.exists(lib):
+        pytest.skip("libsfmfeat.so not built")
+    names = set(m.decode() for m in re.findall(rb"SFMFEAT_[A-Z0-9_]+", open(lib, "rb").read()))
+    assert names, "no switch names found (string scan broken?)"
+    assert names <= set(PRODUCT_SWITCHES), sorted(names - set(PRODUCT_SWITCHES))
+    for diag in ("SFMFEAT_HARRIS_MF", "SFMFEAT_HARRIS_PP", "SFMFEAT_HARRIS_NPAIR", "SFMFEAT_NMS_BAND",
+                 "SFMFEAT_SELECT_CALLER", "SFMFEAT_RERANK8_MAX", "SFMFEAT_MATCH_UNITS"):
+        assert diag not in names

@@ -83,6 +83,26 @@ def test_descriptors_vs_golden_all_widths():
         assert np.array_equal(bits(d), bits(od)), (fw, rotate)
 
 
+@pytest.mark.parametrize("fw", [24, 32, 48])
+@pytest.mark.parametrize("rotate", [True, False])
+def test_wide_feature_width_describe_fallback_vs_oracle(fw, rotate):
+    """Feature widths above the quad kernel's limit (22) run k_describe, one wavefront per
+    keypoint (describe.hip): its descriptors are bit-identical to the oracle's
+    (ScaleRotInvSIFT.py:33-87 / NaiveSIFT.py:122-173 at windows of 24-48 px, where the 4 x 4
+    cells cover only the window's top-left 16 x 16)."""
+    img = synth.make_frame(160, 224, 31, fw)
+    pp = dict(P_MAIN, num_interest_points=150, feature_width=fw)
+    if rotate:
+        obj = ScaleRotInvSIFT(img, dict(pp, pyramid_level=1))
+    else:
+        obj = NaiveSIFT(img, pp)
+    x, y = obj.detect_keypoints()
+    d = obj.extract_descriptors()
+    assert len(x) > 20
+    od = O.descriptors(img, x, y, fw, rotate)
+    assert np.array_equal(bits(d), bits(od)), (fw, rotate)
+
+
 EXTRACT_FIXTURES = ["extract_small_scalerot.npz", "extract_small_pmain.npz", "extract_small_naive.npz",
                     "extract_small_defaults.npz", "extract_c1_640x480_pmain.npz", "extract_c2_1080p_poct.npz"]
 
@@ -409,16 +429,16 @@ def test_configs2_workload_1080p_all_pairs_vs_oracle():
         assert_matches_equal(om[p][0], om[p][1], mm[p, :k], mc[p, :k])
 
 
-def test_matcher_work_units_ragged_counts_many_pairs():
-    """The sweep's work units (k_match_units): ragged per-image counts around the 256-row
-    query blocks (0, 1, 255, 256, 257, 511, 513, ...), so pairs have 0-3 blocks and some none,
-    and 1,128 pairs (the unit scan's second 1,024-pair chunk); every pair equals the oracle
-    (n2 < 2: the reference's IndexError, nmatch -1)."""
-    torch = pytest.importorskip("torch")
+RAGGED_NS = [0, 1, 2, 127, 128, 129, 255, 256, 257, 300, 511, 513, 700, 64, 400, 5, 260, 768]
+
+
+def ragged_match_case():
+    """The ragged work-unit case of test_matcher_work_units_ragged_counts_many_pairs: its
+    slot table (host copy), counts, pairs and the GPU matcher's outputs."""
+    import torch
     from sfmfromscratch_amd.pipeline import BatchMatcher, SlotTable, all_pairs
-    ns = [0, 1, 2, 255, 256, 257, 300, 511, 513, 700, 64, 129, 400, 5, 260, 768]
     S, cap = 48, 768
-    counts = [ns[i % len(ns)] for i in range(S)]
+    counts = [RAGGED_NS[i % len(RAGGED_NS)] for i in range(S)]
     base, hb = synth.make_descriptor_table(cap, 4242)
     slots = SlotTable(torch, S, cap, "cuda")
     host = np.zeros((S, cap, 128), np.float32)
@@ -429,10 +449,38 @@ def test_matcher_work_units_ragged_counts_many_pairs():
     slots.desc.copy_(torch.from_numpy(host))
     slots.count.copy_(torch.tensor(counts, dtype=torch.int32))
     pairs_np = all_pairs(S)
-    assert len(pairs_np) > 1024
     mm, mc, nm = BatchMatcher(0.85).match(slots, torch.from_numpy(pairs_np).cuda())
     torch.cuda.synchronize()
-    mm, mc, nm = mm.cpu().numpy(), mc.cpu().numpy(), nm.cpu().numpy()
+    return host, counts, pairs_np, mm.cpu().numpy(), mc.cpu().numpy(), nm.cpu().numpy()
+
+
+@pytest.mark.parametrize("stage", ["3", "1"])
+def test_matcher_work_units_ragged_counts_many_pairs(stage, tmp_path):
+    """The sweep's work units (k_match_units): ragged per-image counts around the query blocks
+    of both sweep forms — 128 rows (the default half-CU form, SFMFEAT_MATCH_STAGE 3: 0-6 blocks
+    per pair) and 256 rows (the one-CU form, SFMFEAT_MATCH_STAGE=1, run in a child process since
+    the library reads the switch once): counts 0, 1, 127, 128, 129, 255, 256, 257, 511, 513, ...,
+    so some pairs have no block, and 1,128 pairs (the unit scan's second 1,024-pair chunk); every
+    pair equals the oracle (n2 < 2: the reference's IndexError, nmatch -1)."""
+    pytest.importorskip("torch")
+    if stage == "3":
+        host, counts, pairs_np, mm, mc, nm = ragged_match_case()
+    else:
+        import os
+        import subprocess
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        path = str(tmp_path / "ragged.npz")
+        code = ("import sys, numpy as np; sys.path.insert(0, %r); from tests import test_gpu_parity as t; "
+                "h, c, p, mm, mc, nm = t.ragged_match_case(); np.savez(%r, host=h, counts=np.array(c), pairs=p, "
+                "mm=mm, mc=mc, nm=nm)" % (root, path))
+        r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SFMFEAT_MATCH_STAGE=stage), cwd=root,
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        z = np.load(path)
+        host, counts, pairs_np, mm, mc, nm = (z["host"], [int(v) for v in z["counts"]], z["pairs"], z["mm"],
+                                              z["mc"], z["nm"])
+    assert len(pairs_np) > 1024
 
     def ref(pq):
         i, j = pq

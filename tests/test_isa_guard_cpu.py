@@ -32,7 +32,8 @@ FORBIDDEN = [("v_pk_fma_f32", re.compile(r"op_sel:\[[01],1,[01]\]")),
              ("v_pk_add_f32", re.compile(r"op_sel:\[[01],1\]"))]
 
 
-def _device_asm(tmp_path) -> str:
+def _device_elfs(tmp_path) -> list:
+    """The library's device code objects (one per translation unit), unbundled into tmp_path."""
     objcopy = shutil.which("objcopy")
     bundler, objdump = os.path.join(LLVM, "clang-offload-bundler"), os.path.join(LLVM, "llvm-objdump")
     if not (os.path.exists(LIB) and objcopy and os.path.exists(bundler) and os.path.exists(objdump)):
@@ -49,9 +50,45 @@ def _device_asm(tmp_path) -> str:
         b.write_bytes(data[i:j])
         subprocess.run([bundler, "--unbundle", "--type=o", f"--input={b}",
                         "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={e}"], check=True)
-        out.append(subprocess.run([objdump, "-d", "--mcpu=gfx950", str(e)], check=True,
-                                  capture_output=True, text=True).stdout)
-    return "\n".join(out)
+        out.append(str(e))
+    return out
+
+
+def _device_asm(tmp_path) -> str:
+    objdump = os.path.join(LLVM, "llvm-objdump")
+    return "\n".join(subprocess.run([objdump, "-d", "--mcpu=gfx950", e], check=True, capture_output=True,
+                                    text=True).stdout for e in _device_elfs(tmp_path))
+
+
+def _kernel_lds(tmp_path) -> dict:
+    """Static LDS bytes per kernel symbol (.group_segment_fixed_size of the code objects'
+    AMDGPU metadata notes; the keys of each kernel's map print in sorted order, so a kernel's
+    size precedes its .name)."""
+    readelf = os.path.join(LLVM, "llvm-readelf")
+    lds, g = {}, None
+    for e in _device_elfs(tmp_path):
+        notes = subprocess.run([readelf, "--notes", e], check=True, capture_output=True, text=True).stdout
+        for line in notes.splitlines():
+            m = re.search(r"\.group_segment_fixed_size:\s*(\d+)", line)
+            if m:
+                g = int(m.group(1))
+            m = re.search(r"^\s*\.name:\s*(\S+)", line)
+            if m and g is not None:
+                lds[m.group(1)] = g
+                g = None
+    return lds
+
+
+def test_half_cu_sweep_fits_beside_one_harris_workgroup(tmp_path):
+    """The half-CU matcher sweep (k_match_mfma<3>) exists to share a CU with one k_harris
+    workgroup of the other batch: their LDS together must fit the CU's 160 KB.
+    Read from the built code objects, so a Harris form that grows its LDS (e.g. another
+    histogram copy) cannot silently lose the co-residency."""
+    lds = _kernel_lds(tmp_path)
+    harris = [v for k, v in lds.items() if k.startswith("_ZN3sfm8k_harrisILi7ELb1ELi0ELi0E")]
+    sweep3 = [v for k, v in lds.items() if k.startswith("_ZN3sfm12k_match_mfmaILi3ELi0E")]
+    assert len(harris) == 1 and len(sweep3) == 1, (harris, sweep3)
+    assert harris[0] + sweep3[0] <= 160 * 1024, f"k_harris {harris[0]} B + half-CU sweep {sweep3[0]} B > 160 KB"
 
 
 def test_no_packed_fma_with_src1_high_half_select(tmp_path):
