@@ -344,6 +344,12 @@ float sfm_debug_harris_stamps(int32_t device, int32_t abl, int32_t B, int32_t H,
  * then u64 [1024 workgroups][4]: start / end realtime, __smid(), pair | row0 << 32. */
 int64_t sfm_debug_match_stamps(uint64_t* out, int64_t cap);
 
+/* Exchange emulation for a single-GPU rehearsal of the multi-GPU job (bench.py
+ * --emulate-exchange): copy `bytes` from src to dst (device pointers, 16-B aligned) on
+ * `stream` with exactly `workgroups` persistent 256-thread workgroups — the launch shape of a
+ * collective kernel (one workgroup per channel) receiving the same bytes. */
+int32_t sfm_copy_wg(void* dst, const void* src, int64_t bytes, int32_t workgroups, void* stream);
+
 /* Keypoint selection of the context's last extraction (synchronises the device): planes
  * (image x level) that took the exact-median path, and planes in total.  The default
  * certified select decides the others from the Harris histogram alone. */

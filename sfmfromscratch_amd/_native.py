@@ -77,6 +77,7 @@ SIGNATURES = {
     "sfm_debug_harris_stamps": (ctypes.c_float, [ctypes.c_int32] * 6 + [ctypes.c_void_p, ctypes.c_int64]),
     "sfm_debug_match_stamps": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int64]),
     "sfm_debug_select_stats": (ctypes.c_int32, [_vp, _i32p, _i32p]),
+    "sfm_copy_wg": (ctypes.c_int32, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, _vp]),
 
     "sfm_debug_copy_level": (ctypes.c_int32, [_vp, ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
     "sfm_debug_atan2": (ctypes.c_int32, [ctypes.c_int32, _fp, _fp, _fp, ctypes.c_int64]),
@@ -359,6 +360,11 @@ class Context:
                        stream: int = 0):
         check(self.lib.sfm_match_prep_dev(self.handle, desc_ptr, count_ptr, nimg, cap, slot_lo, slot_n,
                                           stream or None), self.handle)
+
+
+def copy_wg(dst_ptr: int, src_ptr: int, nbytes: int, workgroups: int, stream: int = 0):
+    """sfm_copy_wg: a `workgroups`-workgroup device copy on `stream` (exchange emulation)."""
+    check(load_library().sfm_copy_wg(dst_ptr, src_ptr, int(nbytes), int(workgroups), stream or None))
 
 
 def debug_atan2(y: np.ndarray, x: np.ndarray, device: int = 0) -> np.ndarray:

@@ -19,6 +19,18 @@ __global__ void k_debug_atan2(const float* __restrict__ y, const float* __restri
   if (i < n) out[i] = svml_atan2f(y[i], x[i]);
 }
 
+// Exchange emulation (bench.py --emulate-exchange): a grid-stride 16-B copy run by exactly
+// gridDim.x persistent workgroups, the shape of a collective's kernel (one workgroup per
+// channel), so its CU residency and HBM traffic compete with extraction the way an all-gather
+// of the same bytes would on the GPU that receives them.
+__global__ void __launch_bounds__(256) k_copy_wg(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n16,
+                                                 const uint8_t* __restrict__ src_b, uint8_t* __restrict__ dst_b,
+                                                 int64_t tail) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+  if (blockIdx.x == 0 && threadIdx.x < tail) dst_b[threadIdx.x] = src_b[threadIdx.x];
+}
+
 }  // namespace sfm
 
 extern "C" {
@@ -56,13 +68,15 @@ int32_t sfm_debug_harris(int32_t device, const float* gauss, int32_t gs, double 
   unsigned long long* d_cnt = nullptr;
   uint64_t* d_cand = nullptr;
   int32_t rc = SFM_OK;
-  if (hipMalloc(&d_img, n * 4) || hipMalloc(&d_R, n * 4) || hipMalloc(&d_g, 4 * gs * gs) ||
+  std::vector<float> taps(harris_taps_floats(gs));
+  harris_taps_build(gauss, gs, taps.data());
+  if (hipMalloc(&d_img, n * 4) || hipMalloc(&d_R, n * 4) || hipMalloc(&d_g, 4 * taps.size()) ||
       hipMalloc(&d_hist, 4 * kMedBins1) || hipMalloc(&d_list, n * 4) || hipMalloc(&d_med, sizeof(MedianState)) ||
       hipMalloc(&d_cnt, 16 * kCounterStride) || hipMalloc(&d_cand, n * 8)) {
     rc = SFM_EDEVICE;
   } else {
     (void)hipMemcpy(d_img, img, n * 4, hipMemcpyHostToDevice);
-    (void)hipMemcpy(d_g, gauss, 4 * gs * gs, hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_g, taps.data(), 4 * taps.size(), hipMemcpyHostToDevice);
     (void)hipMemset(d_hist, 0, 4 * kMedBins1);
     (void)hipMemset(d_cnt, 0, 16 * kCounterStride);
     launch_harris(d_img, d_R, d_hist, 1, H, W, d_g, gs, (float)alpha, SelectScan{nullptr, nullptr, nullptr, 0, 0},
@@ -143,7 +157,7 @@ float sfm_debug_harris_stamps(int32_t device, int32_t abl, int32_t B, int32_t H,
   int64_t n = (int64_t)B * H * W;
   float *d_img = nullptr, *d_R = nullptr, *d_g = nullptr;
   uint32_t* d_hist = nullptr;
-  if (hipMalloc(&d_img, n * 4) || hipMalloc(&d_R, n * 4) || hipMalloc(&d_g, 4 * 49) ||
+  if (hipMalloc(&d_img, n * 4) || hipMalloc(&d_R, n * 4) || hipMalloc(&d_g, 4 * harris_taps_floats(7)) ||
       hipMalloc(&d_hist, (size_t)B * 4 * kMedBins1))
     return -1.0f;
   std::vector<float> h(n);
@@ -152,10 +166,12 @@ float sfm_debug_harris_stamps(int32_t device, int32_t abl, int32_t B, int32_t H,
     x = x * 1664525u + 1013904223u;
     h[i] = (float)(x >> 24) / 255.0f;
   }
-  float g[49];
-  for (int i = 0; i < 49; ++i) g[i] = 1.0f / 49.0f;
+  float g0[49];
+  for (int i = 0; i < 49; ++i) g0[i] = 1.0f / 49.0f;
+  std::vector<float> g(harris_taps_floats(7));
+  harris_taps_build(g0, 7, g.data());
   (void)hipMemcpy(d_img, h.data(), n * 4, hipMemcpyHostToDevice);
-  (void)hipMemcpy(d_g, g, 4 * 49, hipMemcpyHostToDevice);
+  (void)hipMemcpy(d_g, g.data(), 4 * g.size(), hipMemcpyHostToDevice);
   (void)hipMemset(d_hist, 0, (size_t)B * 4 * kMedBins1);
   // the kernel skips the stamps of workgroups whose slots lie beyond cap (the grid is
   // chosen inside the launcher, so the caller cannot size cap exactly)
@@ -167,6 +183,17 @@ float sfm_debug_harris_stamps(int32_t device, int32_t abl, int32_t B, int32_t H,
   void* bufs[] = {d_img, d_R, d_g, d_hist};
   for (void* b : bufs) (void)hipFree(b);
   return ms;
+}
+
+int32_t sfm_copy_wg(void* dst, const void* src, int64_t bytes, int32_t workgroups, void* stream) {
+  if (bytes < 0 || workgroups < 1 || (bytes > 0 && (!dst || !src))) return SFM_EINVAL;
+  if ((((uintptr_t)dst) | ((uintptr_t)src)) & 15) return SFM_EINVAL;
+  if (bytes == 0) return SFM_OK;
+  const int64_t n16 = bytes / 16, tail = bytes - 16 * n16;
+  hipLaunchKernelGGL(k_copy_wg, dim3((unsigned)workgroups), dim3(256), 0, (hipStream_t)stream,
+                     (const uint4*)src, (uint4*)dst, n16, (const uint8_t*)src + 16 * n16, (uint8_t*)dst + 16 * n16,
+                     tail);
+  return hipGetLastError() == hipSuccess ? SFM_OK : SFM_EDEVICE;
 }
 
 // The matcher sweep's per-wave clock stamps (diagnostic build, SFMFEAT_MATCH_ABL=32).

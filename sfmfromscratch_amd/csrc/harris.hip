@@ -41,6 +41,11 @@ constexpr int kHarrisProductPlanes = 0;
 constexpr int kHarrisMfma = 0;
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+// the window's tap pairs, read through the constant address space: wave-uniform scalar loads
+// (s_load_dwordx*) into SGPRs that the packed fmas take as an operand — no LDS reads and no
+// VGPRs for the 49 taps (round 5 read them as LDS broadcasts: 8 ds_read_b128 per gradient row
+// per thread into 32 VGPRs)
+typedef __attribute__((address_space(4))) const f32x2 cf32x2;
 
 // acc = (k.x, k.y) * (v[H], v[H]) + acc : one v_pk_fma_f32 (two IEEE fmas, each bitwise
 // fmaf) with the product value broadcast to both halves by op_sel — no register shuffles.
@@ -62,14 +67,16 @@ __device__ __forceinline__ void pk_fma_bcast(f32x2& acc, f32x2 k, f32x2 v) {
   acc.y = __builtin_fmaf(k.y, v[H], acc.y);
   return;
 #endif
+  // k (the tap pair) is wave-uniform and lives in an SGPR pair (one scalar operand: the
+  // constant-bus limit)
   if constexpr (H == 0)
-    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "v"(k), "v"(v));
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(acc) : "s"(k), "v"(v));
 #ifdef SFM_HARRIS_SRC1_HI
   else
-    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(k), "v"(v));
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "s"(k), "v"(v));
 #else
   else
-    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(v), "v"(k));
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,1,1]" : "+v"(acc) : "v"(v), "s"(k));
 #endif
 }
 
@@ -210,13 +217,9 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   // shifted by half the banks) where the LDS budget of WPC workgroups per CU allows, halving
   // the same-address serialisation of one wave's LDS adds
   constexpr int kHistCopy = kMedBins1 + 32;
-  constexpr int kLdsRest = 4 * (NPL * PH * PWP + (PP ? 0 : IH * IWP)) +
-                           8 * (KS + 2 * NPAIR - 1) * NPAIR * (KS + (KS & 1)) + 1024;
+  constexpr int kLdsRest = 4 * (NPL * PH * PWP + (PP ? 0 : IH * IWP)) + 1024;
   constexpr int NHC = kLdsRest + 8 * kHistCopy <= 163840 / HarrisShape<F>::WPC ? 2 : 1;
   __shared__ uint32_t s_hist[NHC * kHistCopy];
-  // tap pairs per gradient row r and row pair p: (g[r-2p][j], g[r-2p-1][j]), 0 where the
-  // tap row does not exist; read as uniform LDS broadcasts (49 taps in SGPRs spill)
-  __shared__ __attribute__((aligned(16))) f32x2 s_tp[KS + 2 * NPAIR - 1][NPAIR][KS + (KS & 1)];
   __shared__ uint32_t s_last, s_red[10];
 
   const int tid = threadIdx.x;
@@ -240,11 +243,6 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   const float* img = lvl + (int64_t)b * H * W;
   float* Rp = Rout + (int64_t)b * H * W;
   for (int i = tid; i < NHC * kHistCopy; i += NT) s_hist[i] = 0u;
-  for (int i = tid; i < (KS + 2 * NPAIR - 1) * NPAIR * KS; i += NT) {
-    const int r = i / (NPAIR * KS), p = (i / KS) % NPAIR, j = i % KS;
-    const int i0 = r - 2 * p, i1 = i0 - 1;
-    s_tp[r][p][j] = f32x2{(i0 >= 0 && i0 < KS) ? gk[i0 * KS + j] : 0.0f, (i1 >= 0 && i1 < KS) ? gk[i1 * KS + j] : 0.0f};
-  }
   const int lane = tid & 63, wv = tid >> 6;
   uint32_t* const s_hc = s_hist + (NHC == 2 ? (lane & 1) * kHistCopy : 0);
   // MFMA window: the banded tap operand A(dy, s), lane 4b+i: g[dy][s - i] (0 off the band).
@@ -272,10 +270,27 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   f32x4 t4[VEC ? NIMG : 1];
   float t1[VEC ? 1 : NIMG];
   uint64_t okmask = 0;
+  // the interior form's element offsets inside the tile window (row * W + column), fixed per
+  // thread: a tile whose window lies wholly inside the image loads from one scalar base plus
+  // these, with no per-element bounds (the image-tile copy below stores it unmasked too)
+  int eoff[VEC ? NIMG : 1];
+  if constexpr (VEC) {
+#pragma unroll
+    for (int k = 0; k < NIMG; ++k) {
+      const int e = tid + NT * k, iy = e / IW4;
+      eoff[k] = e < IH * IW4 ? iy * W + 4 * (e - iy * IW4) : 0;
+    }
+  }
   auto prefetch = [&](int tile) {
     const int gx0 = (tile % tiles_x) * kHT - XA;
     const int gy0 = (tile / tiles_x) * TH - GA - 1;
     okmask = 0;
+    if (VEC && gx0 >= 0 && gx0 + IWP <= W && gy0 >= 0 && gy0 + IH <= H) {
+      const float* tb = img + (int64_t)gy0 * W + gx0;
+#pragma unroll
+      for (int k = 0; k < NIMG; ++k) t4[VEC ? k : 0] = *reinterpret_cast<const f32x4*>(tb + (VEC ? eoff[k] : 0));
+      return;
+    }
     if constexpr (VEC) {
 #pragma unroll
       for (int k = 0; k < NIMG; ++k) {
@@ -314,6 +329,11 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     }
     const int tx0 = (tile % tiles_x) * kHT;
     const int ty0 = (tile / tiles_x) * TH;
+    // tap pairs (harris_taps_build): pair (d, j) = (g[d][j], g[d-1][j]) for d = 0..KS, a
+    // missing tap row 0.  The pointer is laundered once per tile so the compiler re-issues the
+    // scalar loads per gradient row instead of hoisting all (KS+1) x KS pairs into SGPRs
+    const cf32x2* tp = (const cf32x2*)(gk + kHarrisPairOff);
+    asm volatile("" : "+s"(tp));
     if constexpr (ABL != 4) __syncthreads();  // the previous tile's LDS reads are done
     // 0. the prefetched image tile -> LDS, then start fetching the next tile (a tile whose
     //    whole image window lies inside the image stores its loads unmasked)
@@ -616,15 +636,16 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
           P[2][m] = X[m] * Y[m];
         }
       }
-      f32x2 T[NPAIR][KS + (KS & 1)];
+      f32x2 T[NPAIR][KS];
+      asm volatile("" : "+s"(tp));  // this row's pairs are loaded here, not hoisted with every row's
 #pragma unroll
-      for (int p = 0; p < NPAIR; ++p)
+      for (int p = 0; p < NPAIR; ++p) {
+        const int d = r - 2 * p;  // tap rows (d, d - 1) of the pair's two output rows
+        if (d >= 0 && d <= KS) {
 #pragma unroll
-        for (int j2 = 0; j2 < (KS + 1) / 2; ++j2) {
-          const float4 t = *reinterpret_cast<const float4*>(&s_tp[r][p][2 * j2]);
-          T[p][2 * j2] = f32x2{t.x, t.y};
-          T[p][2 * j2 + 1] = f32x2{t.z, t.w};
+          for (int j = 0; j < KS; ++j) T[p][j] = tp[d * KS + j];
         }
+      }
 #pragma unroll
       for (int p = 0; p < NPAIR; ++p) {
         const int i0 = r - 2 * p, i1 = r - 2 * p - 1;  // tap rows of the pair's two rows
@@ -667,6 +688,25 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     //    inside the plane counts and stores without per-pixel bounds
     auto epilogue = [&](auto fullc) {
       constexpr bool FULL = decltype(fullc)::value;
+      // R of both rows of each accumulator pair at once: the same IEEE operations as the
+      // per-pixel form (t1 = sxx*syy, t2 = sxy*sxy, det = t1 - t2, tr = sxx + syy, tr2 =
+      // tr*tr, at = alpha*tr2, R = det - at), as plain v_pk_mul / v_pk_add (no op_sel)
+      f32x2 Rpk[NPAIR][4];
+      const f32x2 al2 = {alpha, alpha};
+#pragma unroll
+      for (int p = 0; p < NPAIR; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x2 sxx = acc[p][0][q], syy = acc[p][1][q];
+          const f32x2 sxy = HY ? f32x2{macc2[HY ? 2 * p : 0][q], macc2[HY ? 2 * p + 1 : 0][q]} : acc[p][2][q];
+          const f32x2 t1v = sxx * syy;
+          const f32x2 t2v = sxy * sxy;
+          const f32x2 det = t1v - t2v;
+          const f32x2 tr = sxx + syy;
+          const f32x2 tr2 = tr * tr;
+          const f32x2 at = al2 * tr2;
+          Rpk[p][q] = det - at;
+        }
 #pragma unroll
       for (int o = 0; o < RPT; ++o) {
         const int gy = ty0 + RPT * rq + o;
@@ -674,15 +714,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
         float Rq[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float sxx = acc[o >> 1][0][q][o & 1], syy = acc[o >> 1][1][q][o & 1],
-                      sxy = HY ? macc2[HY ? o : 0][q] : acc[o >> 1][2][q][o & 1];
-          const float t1v = sxx * syy;
-          const float t2v = sxy * sxy;
-          const float det = t1v - t2v;
-          const float tr = sxx + syy;
-          const float tr2 = tr * tr;
-          const float at = alpha * tr2;
-          Rq[q] = det - at;
+          Rq[q] = Rpk[o >> 1][q][o & 1];
           if (ABL != 1)
             atomicAdd(&s_hc[fkey(Rq[q]) >> (32 - kMedBits1)], (FULL || (gy < H && gx0 + q < W)) ? 1u : 0u);
         }
@@ -756,6 +788,19 @@ static int harris_plan(HarrisLevels& g, int B, int slots) {
     wg += g.l[k].nwg;
   }
   return wg;
+}
+
+size_t harris_taps_floats(int ks) { return (size_t)kHarrisPairOff + 2 * (size_t)(ks + 1) * ks; }
+
+void harris_taps_build(const float* g, int ks, float* out) {
+  for (size_t i = 0; i < harris_taps_floats(ks); ++i) out[i] = 0.0f;
+  for (int i = 0; i < ks * ks; ++i) out[i] = g[i];
+  float* tp = out + kHarrisPairOff;
+  for (int d = 0; d <= ks; ++d)
+    for (int j = 0; j < ks; ++j) {
+      tp[2 * (d * ks + j)] = d < ks ? g[d * ks + j] : 0.0f;
+      tp[2 * (d * ks + j) + 1] = d >= 1 ? g[(d - 1) * ks + j] : 0.0f;
+    }
 }
 
 static int env_int(const char* name, int dflt) {  // product switch (tests/test_gpu_switches.py)

@@ -233,6 +233,12 @@ struct HarrisLevels {
 };
 void launch_harris_levels(const HarrisLevels& g, int B, const float* d_gauss, int ks, float alpha,
                           hipStream_t st);
+// The Harris launches' tap buffer (d_gauss above): the ks x ks Gaussian taps (row-major) at 0,
+// then from float kHarrisPairOff the window's tap pairs (g[d][j], g[d-1][j]) for d = 0..ks,
+// j < ks (a missing tap row is 0), which the kernel reads as wave-uniform scalar loads.
+constexpr int kHarrisPairOff = 256;
+size_t harris_taps_floats(int ks);
+void harris_taps_build(const float* g, int ks, float* out);
 
 int64_t match_stamps_copy(uint64_t* out, int64_t cap);
 // words of the sweep's work-unit list (k_match_units) for P pairs of up to max_rows rows

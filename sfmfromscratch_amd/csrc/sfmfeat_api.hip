@@ -753,8 +753,10 @@ int32_t sfm_ctx_create(int32_t device, const sfm_params* p, sfm_ctx** out) {
     delete c;
     return SFM_EDEVICE;
   }
-  if (ensure(c, c->d_gauss, sizeof(float) * gs * gs) ||
-      hipMemcpy(c->d_gauss.p, c->gauss, sizeof(float) * gs * gs, hipMemcpyHostToDevice) != hipSuccess) {
+  std::vector<float> taps(harris_taps_floats(gs));
+  harris_taps_build(c->gauss, gs, taps.data());
+  if (ensure(c, c->d_gauss, sizeof(float) * taps.size()) ||
+      hipMemcpy(c->d_gauss.p, taps.data(), sizeof(float) * taps.size(), hipMemcpyHostToDevice) != hipSuccess) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->aux) (void)hipStreamDestroy(c->aux);
     for (hipEvent_t e : c->ev) (void)hipEventDestroy(e);
