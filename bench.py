@@ -294,6 +294,12 @@ def main():
     ap.add_argument("--same-batch", action="store_true",
                     help="c2: submit the same 32 frames every step (default: two distinct batches alternate, so "
                          "no step re-reads the frames of the step before it)")
+    ap.add_argument("--emulate-exchange", type=int, default=0, metavar="WG",
+                    help="c4 at one GPU: a single-GPU rehearsal of one rank of an --emulate-world-rank job: after "
+                         "each chunk's extraction a WG-workgroup device copy of the bytes that rank would receive "
+                         "(count-compacted all-gather) on a high-priority stream, the chunk's pairs waiting for it; "
+                         "reports the extraction slowdown and the hidden fraction of the emulated exchange")
+    ap.add_argument("--emulate-world", type=int, default=8)
     ap.add_argument("--verify", action="store_true",
                     help="c4: after the timed run, re-extract a sample of frames and re-match a sample of this "
                          "rank's pairs with the plain (unchunked) calls and require bit-equal results")
@@ -862,6 +868,10 @@ def run_gather(args, torch, dist, dev, rank, world):
             log(f"rank 0 alone: {n_global} frames in {t1 * 1e3:.2f} ms")
         dist.barrier()
 
+    if args.emulate_exchange > 0:
+        if world != 1:
+            raise SystemExit("--emulate-exchange is a single-GPU rehearsal (run it with --gpus 1)")
+        return run_emulated_exchange(args, torch, dev, D, plan, frames_of(rank, S), timed, n_global)
     job = D.ChunkedGatherJob(P_OCT, RATIO, plan, rank, H, W, dist=dist if world > 1 else None,
                              inflight=args.inflight, exchange=args.exchange, device=dev.index)
     frames = frames_of(rank, S)
@@ -981,6 +991,57 @@ def run_gather(args, torch, dist, dev, rank, world):
             sys.exit(4)
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_emulated_exchange(args, torch, dev, D, plan, frames, timed, n_global):
+    """--emulate-exchange WG (configs[3] readiness on one GPU): the job of one
+    rank of an N-rank run (--frames = its shard, e.g. 256 = 2,048 / 8), first alone (T_compute),
+    then with an emulated exchange per chunk (T_emu): a WG-workgroup copy of the bytes the rank
+    would receive — (N - 1) x 32 frames x (M rows x 520 B + 4), M the largest keypoint count —
+    on a high-priority stream, the chunk's pairs waiting for it (distributed.ChunkedGatherJob
+    `emulate`).  hidden_fraction = 1 - (T_emu - T_compute) / T_copies_alone.  It measures the
+    collective's CU and HBM contention with extraction, not xGMI latency."""
+    job = D.ChunkedGatherJob(P_OCT, RATIO, plan, 0, H, W, inflight=args.inflight, device=dev.index)
+    for _ in range(max(1, args.warmup)):
+        job.run(frames)
+    torch.cuda.synchronize()
+    rows = int(job.table.count.max().item())
+    t_compute = timed(job, frames, args.steps)
+    emu = {"world": args.emulate_world, "workgroups": args.emulate_exchange, "rows": rows}
+    ejob = D.ChunkedGatherJob(P_OCT, RATIO, plan, 0, H, W, inflight=args.inflight, device=dev.index, emulate=emu)
+    for _ in range(max(1, args.warmup)):
+        ejob.run(frames)
+    torch.cuda.synchronize()
+    t_emu = timed(ejob, frames, args.steps)
+    t_alone = ejob.emulated_gather_alone()
+    t_compute2 = timed(job, frames, args.steps)  # again after, against drift
+    t_c = min(t_compute, t_compute2)
+    e = ejob.emulate
+    comm = {"kind": (f"EMULATED exchange on one GPU: per chunk a {e['workgroups']}-workgroup device copy of the "
+                     f"{e['bytes_per_chunk']} B one rank of a {e['world']}-rank job receives (count-compacted rows, "
+                     f"M = {rows}) on a high-priority stream; the chunk's pairs wait for it"),
+            "emulated_world": e["world"], "workgroups": e["workgroups"], "rows": rows,
+            "bytes_per_chunk": e["bytes_per_chunk"], "chunks": plan.C,
+            "copies_alone_ms": round(t_alone * 1e3, 3),
+            "copies_alone_GBps": round(e["bytes_per_chunk"] * plan.C / t_alone / 1e9, 1),
+            "compute_only_ms": round(t_c * 1e3, 3), "compute_only_ms_runs": [round(t_compute * 1e3, 3),
+                                                                             round(t_compute2 * 1e3, 3)],
+            "job_with_emulated_exchange_ms": round(t_emu * 1e3, 3),
+            "extraction_slowdown": round(t_emu / t_c, 4),
+            "hidden_fraction": round(min(1.0, max(0.0, 1.0 - (t_emu - t_c) / t_alone)), 4),
+            "hidden_note": "1 - (T_emu - T_compute) / T_copies_alone"}
+    emit({
+        "metric": "DIAGNOSTIC single-GPU rehearsal (emulated exchange), not a multi-GPU measurement: "
+                  "images/sec detect+describe+match, 1080p, one rank's shard",
+        "value": round(plan.S / t_emu, 2), "unit": "images/sec", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(t_emu * 1e3, 3), "higher_is_better": True,
+        "scaling": args.scaling, "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (deterministic integer-generated textured 1080p frames, device-resident float32 gray)",
+        "config": {"workload": f"BASELINE configs[3] readiness: one rank's {plan.S}-frame shard of an "
+                               f"{e['world']}-rank job, 32-frame chunks, emulated all-gather per chunk",
+                   "frames_per_gpu": plan.S, "chunk": plan.chunk, "parallelism": "single GPU (emulation)",
+                   "batches_in_flight": args.inflight, "n_global_arg": n_global},
+        "collective": comm, "roofline": None, "cpu_baseline": None}, args)
 
 
 def verify_gather_job(args, torch, dist, dev, job, frame_of, world, rank):

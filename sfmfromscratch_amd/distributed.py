@@ -345,7 +345,7 @@ class ChunkedGatherJob:
     def __init__(self, extractor_params: dict | None, ratio: float, plan: GatherPlan, rank: int, H: int, W: int,
                  dist=None, inflight: int = 2, exchange: str = "allgather", device: int = 0, group=None,
                  coalesce: bool | None = None, keep_all_results: bool = False, compact: bool | None = None,
-                 lane_streams: str | None = None):
+                 lane_streams: str | None = None, emulate: dict | None = None):
         import torch
         from .pipeline import BatchExtractor, BatchMatcher, SlotTable
         self.torch, self.plan, self.rank, self.dist, self.group = torch, plan, rank, dist, group
@@ -421,6 +421,25 @@ class ChunkedGatherJob:
         self.pairs_matched = self.rank_pairs_n
         self.slot_bytes = cap * (128 * 4 + 2 * 4) + 4
         self.sent_ck = None
+        # Exchange emulation on one GPU (bench.py --emulate-exchange; world 1 only): after each
+        # chunk's extraction, a copy of the bytes one rank of an `emulate["world"]`-rank job
+        # receives for that chunk — (world - 1) x chunk frames x (rows x 520 B + 4), the
+        # count-compacted all-gather's payload — on a high-priority stream by
+        # `emulate["workgroups"]` persistent workgroups (a collective kernel's launch shape), and
+        # the chunk's pairs wait for it as they wait for the real gather.  It reproduces the
+        # collective's CU residency and local HBM traffic beside extraction, not xGMI latency.
+        self.emulate = None
+        if emulate:
+            if world != 1:
+                raise ValueError("exchange emulation runs at world size 1")
+            ew, wg = int(emulate.get("world", 8)), int(emulate.get("workgroups", 32))
+            rows = int(emulate.get("rows") or cap)
+            nbytes = (ew - 1) * Bx * (rows * (128 * 4 + 2 * 4) + 4)
+            nbytes = (nbytes + 15) // 16 * 16
+            self.emulate = {"world": ew, "workgroups": wg, "rows": rows, "bytes_per_chunk": nbytes,
+                            "src": torch.zeros(nbytes // 4, dtype=torch.float32, device=dev),
+                            "dst": torch.empty(nbytes // 4, dtype=torch.float32, device=dev),
+                            "stream": torch.cuda.Stream(device=dev, priority=-1)}
 
     def _new_out(self, P):
         torch, cap, dev = self.torch, self.cap, self.dev
@@ -523,6 +542,10 @@ class ChunkedGatherJob:
                         halo_exchange(dist, self.table, plan.S, rank, world, self.group)
                 elif world == 1:
                     ln["ex"].extract(frames[l0:l0 + bc], out=self._view(self.table, plan.chunk_base(c), bc))
+                    if self.emulate is not None and exchange:
+                        ready = self._emulated_gather(ln["stream"])
+                        match_chunk(c, None, ln, ready=ready)
+                        continue
                 else:
                     ln["ex"].extract(frames[l0:l0 + bc], out=self._view(ln["slots"], 0, bc))
                     if record_sent:
@@ -566,6 +589,32 @@ class ChunkedGatherJob:
                                    prepped=True)
             self.pairs_matched = len(mine)
             self.last_all_pairs = sp
+
+    def _emulated_gather(self, after) -> "object":
+        """One chunk's emulated gather on the emulation stream after `after`; its end event."""
+        from ._native import copy_wg
+        torch, e = self.torch, self.emulate
+        es = e["stream"]
+        es.wait_stream(after)
+        copy_wg(e["dst"].data_ptr(), e["src"].data_ptr(), e["bytes_per_chunk"], e["workgroups"], es.cuda_stream)
+        done = torch.cuda.Event()
+        done.record(es)
+        return done
+
+    def emulated_gather_alone(self, reps: int = 3) -> float:
+        """Seconds per job of the emulated exchange's copies alone (C chunks, nothing else on
+        the GPU)."""
+        import time
+        torch = self.torch
+        cur = torch.cuda.current_stream()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            for _c in range(self.plan.C):
+                self._emulated_gather(cur)
+        self.emulate["stream"].synchronize()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
 
     def gathered_bytes(self) -> tuple[int, int]:
         """(bytes each rank received in the last run's row gathers, the same at full slot
