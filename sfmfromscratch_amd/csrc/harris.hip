@@ -213,10 +213,12 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
   __shared__ __attribute__((aligned(16))) float s_pl[NPL * PH * PWP + (PP ? 0 : IH * IWP)];
   float (*const s_g)[PH][PWP] = reinterpret_cast<float (*)[PH][PWP]>(s_pl);
   float (*const s_img)[IWP] = reinterpret_cast<float (*)[IWP]>(s_pl + (PP ? 0 : NPL * PH * PWP));
-  // digit-1 histogram, flushed once per workgroup: two copies (even / odd lanes, the second
-  // shifted by half the banks) where the LDS budget of WPC workgroups per CU allows, halving
-  // the same-address serialisation of one wave's LDS adds
-  constexpr int kHistCopy = kMedBins1 + 32;
+  // digit-1 histogram, flushed once per workgroup: two copies (even / odd lanes) where the LDS
+  // budget of WPC workgroups per CU allows, halving the same-address serialisation of one
+  // wave's LDS adds; the second copy is shifted by 16 words, half of the 32 banks a ds_add_u32
+  // lane group spans, so a bucket's two copies never share a bank (round 6: a 32-word shift
+  // put them on the same bank; L0 alone 397 -> 390 us, profiles/r06_harris_hist_variants.txt)
+  constexpr int kHistCopy = kMedBins1 + 16;
   constexpr int kLdsRest = 4 * (NPL * PH * PWP + (PP ? 0 : IH * IWP)) + 1024;
   constexpr int NHC = kLdsRest + 8 * kHistCopy <= 163840 / HarrisShape<F>::WPC ? 2 : 1;
   __shared__ uint32_t s_hist[NHC * kHistCopy];
