@@ -262,6 +262,14 @@ int32_t sfm_match_pairs_prepped_dev(sfm_ctx* ctx, const float* desc, const int32
  * (SFM_EINVAL after).  BatchPipeline's SFMFEAT_LANE_PRIO=1 gives its first lane the higher
  * priority (an A/B setting; DESIGN_LOG.md §B). */
 int32_t sfm_ctx_stream(sfm_ctx* ctx, void** stream);
+/* sfm_ctx_set_fused_prep: 1 = each batch extraction on this context also writes the matcher's
+ * per-descriptor operands (split-f16 copies, norms, block maxima; sfm_match_prep_dev's work)
+ * from its descriptor kernel, and the next sfm_match_pairs_dev on this context over the same
+ * table (desc, count, cap) preps only the slots beyond the extraction's batch — one launch
+ * fewer per batch (BatchPipeline turns it on for its own tables).  Contract: the
+ * descriptors an extraction wrote are not modified before that match (or
+ * sfm_match_prep_dev is called over them first); 0 (default) = off. */
+int32_t sfm_ctx_set_fused_prep(sfm_ctx* ctx, int32_t on);
 int32_t sfm_ctx_set_serial(sfm_ctx* ctx, int32_t serial);
 int32_t sfm_ctx_set_priority(sfm_ctx* ctx, int32_t priority);
 

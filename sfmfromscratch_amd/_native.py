@@ -64,6 +64,7 @@ SIGNATURES = {
                                                      ctypes.c_int32, ctypes.c_float, _vp, _vp, _vp, _vp]),
     "sfm_ctx_stream": (ctypes.c_int32, [_vp, ctypes.POINTER(_vp)]),
     "sfm_ctx_set_serial": (ctypes.c_int32, [_vp, ctypes.c_int32]),
+    "sfm_ctx_set_fused_prep": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "sfm_ctx_set_priority": (ctypes.c_int32, [_vp, ctypes.c_int32]),
     "sfm_gate_create": (ctypes.c_int32, [ctypes.c_int32, ctypes.POINTER(_vp)]),
     "sfm_gate_destroy": (ctypes.c_int32, [_vp]),
@@ -217,6 +218,10 @@ class Context:
     def set_priority(self, priority: int):
         """HIP priority of the context's streams (lower = higher); before they exist."""
         check(self.lib.sfm_ctx_set_priority(self.handle, int(priority)), self.handle)
+
+    def set_fused_prep(self, on: bool):
+        """Batch extractions write the matcher's operands of their slots (sfm_ctx_set_fused_prep)."""
+        check(self.lib.sfm_ctx_set_fused_prep(self.handle, 1 if on else 0), self.handle)
 
     def set_serial(self, serial: bool):
         """Every extraction stage on the caller's stream (no aux-stream overlap)."""

@@ -312,15 +312,18 @@ void init_describe_attributes(size_t max_lds) {
 bool launch_describe(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp,
                      int kcap, const int32_t* level_counts_all, int level, int L, double scale,
                      int32_t* out_xy, float* out_desc, float* out_conf, int64_t out_cap,
-                     int32_t* out_count, hipStream_t st) {
+                     int32_t* out_count, const MatchOperands& mo, bool* operands_written, hipStream_t st) {
+  if (operands_written) *operands_written = false;
   if (kcap <= 0) return false;
   static const bool one_per_wave = [] {
     const char* v = getenv("SFMFEAT_DESCRIBE");
     return v && v[0] == 'w';  // "wave": the one-keypoint-per-wavefront kernel (A/B timing)
   }();
   if (!one_per_wave && launch_describe_quad(lvl, B, H, W, fw, rotate, kp, kcap, level_counts_all, level,
-                                            scale, out_xy, out_desc, out_conf, out_cap, out_count, L, st))
+                                            scale, out_xy, out_desc, out_conf, out_cap, out_count, L, mo, st)) {
+    if (operands_written) *operands_written = mo.hi != nullptr;
     return out_count != nullptr;
+  }
   size_t lds = describe_lds_bytes(fw, rotate);
   hipLaunchKernelGGL(k_describe, dim3(kcap, B), dim3(64), lds, st, lvl, H, W, fw, rotate, kp, kcap,
                      level_counts_all, level, B, scale, out_xy, out_desc, out_conf, out_cap);

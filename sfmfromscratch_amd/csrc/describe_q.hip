@@ -220,7 +220,8 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
                                                    int kcap, const int32_t* __restrict__ lc_all, int level,
                                                    int B, double scale, int32_t* __restrict__ out_xy,
                                                    float* __restrict__ out_desc, float* __restrict__ out_conf,
-                                                   int64_t out_cap, int32_t* __restrict__ out_count, int L) {
+                                                   int64_t out_cap, int32_t* __restrict__ out_count, int L,
+                                                   MatchOperands mo) {
   using C = Geo<WS, ROT>;
   constexpr int N = C::N, PW = C::PW, NP = C::NP, E = C::E, RN = C::RN, h = WS / 2;
   __shared__ __attribute__((aligned(16))) float s_all[4 * C::G];
@@ -231,6 +232,28 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
     int32_t s = 0;
     for (int l = 0; l < L; ++l) s += lc_all[(int64_t)l * B + b];
     out_count[b] = s;
+  }
+  // fused matcher operands: the last level's launch carries kPadBlocks extra workgroups per
+  // image that write the padding rows [count, capP) (norm2 = +inf, hi = lo = 0), as
+  // k_match_prep does, so the sweep needs no bounds checks
+  const int nkb = (kcap + 3) / 4;
+  if ((int)blockIdx.x >= nkb) {
+    int32_t s = 0;
+    for (int l = 0; l < L; ++l) s += lc_all[(int64_t)l * B + b];
+    const int nt = ((int)gridDim.x - nkb) * 64;
+    for (int64_t r = s + ((int)blockIdx.x - nkb) * 64 + threadIdx.x; r < mo.capP; r += nt) {
+      const int64_t mr = (int64_t)b * mo.capP + r;
+      uint4* hz = reinterpret_cast<uint4*>(mo.hi + mr * 128);
+      uint4* lz = reinterpret_cast<uint4*>(mo.lo + mr * 128);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        hz[q] = make_uint4(0u, 0u, 0u, 0u);
+        lz[q] = make_uint4(0u, 0u, 0u, 0u);
+      }
+      mo.norm2[mr] = INFINITY;
+      mo.rnorm[mr] = 0.0f;
+    }
+    return;
   }
   const int count = kp.count[b];
   const int kbase = blockIdx.x * 4;
@@ -542,6 +565,38 @@ __global__ void __launch_bounds__(64) k_describe_q(const float* __restrict__ lvl
   float4* dst = reinterpret_cast<float4*>(out_desc + slot * 128 + gl * 8);
   dst[0] = make_float4(o[0], o[1], o[2], o[3]);
   dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+  if (mo.hi != nullptr) {
+    // the matcher's operands of this row (k_match_prep's arithmetic: the same hi / lo of each
+    // element; the squared norm summed in double over the row's 16 lanes)
+    const int64_t r = off0 + kpi, mr = (int64_t)b * mo.capP + r;
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    h8 hh, ll;
+    double s = 0.0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float xs = o[t] * kMatchScale;
+      const _Float16 hv16 = (_Float16)xs;
+      const float rr = (xs - (float)hv16) * kMatchLoScale;  // exact difference, exact scaling
+      hh[t] = hv16;
+      ll[t] = (_Float16)rr;
+      s += (double)o[t] * (double)o[t];
+    }
+    *reinterpret_cast<h8*>(mo.hi + mr * 128 + gl * 8) = hh;
+    *reinterpret_cast<h8*>(mo.lo + mr * 128 + gl * 8) = ll;
+    s += rxord<8>(s);
+    s += rxord<4>(s);
+    s += rxord<2>(s);
+    s += rxord<1>(s);
+    if (gl == 0) {
+      const float n2 = (float)s, rn = (float)sqrt(s);
+      mo.norm2[mr] = n2;
+      mo.rnorm[mr] = rn;
+      // per-16-row maxima (non-negative floats order as their bit patterns)
+      float2* pm = mo.pmax + (int64_t)b * (mo.capP / kPrepRows) + r / kPrepRows;
+      atomicMax(reinterpret_cast<unsigned int*>(&pm->x), __float_as_uint(n2));
+      atomicMax(reinterpret_cast<unsigned int*>(&pm->y), __float_as_uint(rn));
+    }
+  }
   if (gl == 0) {
     if (out_conf) out_conf[slot] = kp.conf[ko];
     out_xy[slot * 2 + 0] = (int32_t)((double)x * scale);  // (x * scale).astype(int) :101
@@ -602,10 +657,10 @@ void init_describe_quad_tables() {
 #define SFM_DQ_BODY(WS)                                                                              \
     if (rotate)                                                                                      \
       hipLaunchKernelGGL((dq::k_describe_q<WS, 1>), grid, dim3(64), 0, st, lvl, H, W, kp, kcap, lc,  \
-                         level, B, scale, out_xy, out_desc, out_conf, out_cap, out_count, L);        \
+                         level, B, scale, out_xy, out_desc, out_conf, out_cap, out_count, L, mo);        \
     else                                                                                             \
       hipLaunchKernelGGL((dq::k_describe_q<WS, 0>), grid, dim3(64), 0, st, lvl, H, W, kp, kcap, lc,  \
-                         level, B, scale, out_xy, out_desc, out_conf, out_cap, out_count, L);        \
+                         level, B, scale, out_xy, out_desc, out_conf, out_cap, out_count, L, mo);        \
     return true;
 #define SFM_DQ_CASE(WS) \
   case WS:              \
@@ -613,8 +668,11 @@ void init_describe_quad_tables() {
 
 bool launch_describe_quad(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp, int kcap,
                           const int32_t* lc, int level, double scale, int32_t* out_xy, float* out_desc,
-                          float* out_conf, int64_t out_cap, int32_t* out_count, int L, hipStream_t st) {
-  const dim3 grid((kcap + 3) / 4, B);
+                          float* out_conf, int64_t out_cap, int32_t* out_count, int L, const MatchOperands& mo,
+                          hipStream_t st) {
+  // (+ the padding-row workgroups of the fused matcher operands in the last level's launch)
+  constexpr int kPadBlocks = 8;
+  const dim3 grid((kcap + 3) / 4 + (mo.hi != nullptr && out_count != nullptr ? kPadBlocks : 0), B);
   switch (2 * (fw / 2)) {
     SFM_DQ_CASE(2)
     SFM_DQ_CASE(4)
@@ -635,7 +693,7 @@ bool launch_describe_quad(const float* lvl, int B, int H, int W, int fw, int rot
 #define SFM_DQ_ABL(A)                                                                                     \
   case A:                                                                                                \
     hipLaunchKernelGGL((dq::k_describe_q<18, 1, A>), grid, dim3(64), 0, st, lvl, H, W, kp, kcap, lc, level, \
-                       B, scale, out_xy, out_desc, out_conf, out_cap, out_count, L);                     \
+                       B, scale, out_xy, out_desc, out_conf, out_cap, out_count, L, mo);                     \
     return true;
           SFM_DQ_ABL(1)
           SFM_DQ_ABL(2)

@@ -28,6 +28,24 @@ constexpr int kCounterStride = 32;          // u64 per per-plane atomic counter 
 // matcher sub-launch takes at most 2^kMatchUnitPairBits pairs (match_impl clamps)
 constexpr int kMatchUnitPairBits = 20;
 
+// The matcher's per-descriptor operands (match_mfma.hip): split-f16 copies hi = f16(v * 2^8),
+// lo = f16((v * 2^8 - hi) * 2^11), the squared norm float(sum v^2 in double) and the norm,
+// [img][capP] rows (capP = cap rounded up to 128; padding rows: norm2 = +inf, hi = lo = 0),
+// and per 16-row block the maxima of (norm2, norm) over the valid rows.  k_match_prep writes
+// them from a slot table; an extraction with fused operands (sfm_ctx_set_fused_prep) has the
+// descriptor kernel write them for every row it produces.
+constexpr float kMatchScale = 256.0f;   // operand pre-scale (2^8)
+constexpr float kMatchLoScale = 2048.0f;  // lo part scale (2^11)
+constexpr int kPrepRows = 16;           // rows per (norm2, norm) maxima block
+struct MatchOperands {
+  _Float16* hi;    // nullptr: not written
+  _Float16* lo;
+  float* norm2;
+  float* rnorm;
+  float2* pmax;    // [img][capP / kPrepRows], zeroed by the extraction before its levels
+  int64_t capP;
+};
+
 // Per-plane state of the keypoint selection (NaiveSIFT.py:90-120).
 //
 // Certified select (default): the reference keeps R == window max && R >= median, then the
@@ -299,14 +317,17 @@ void launch_select_levels(const SelectLevels& g, int kcap, int k, int B, int ksi
 bool launch_describe_quad(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp, int kcap,
                           const int32_t* level_counts_all, int level, double scale, int32_t* out_xy,
                           float* out_desc, float* out_conf, int64_t out_cap, int32_t* out_count, int L,
-                          hipStream_t st);
+                          const MatchOperands& mo, hipStream_t st);
 // describe.hip: descriptors of one level written into the output slot table; returns true when
 // the launch also wrote the slot counts (out_count set and the quad kernel took the level),
 // otherwise the caller runs launch_finalize_counts
+// mo.hi set: the quad kernel also writes the matcher operands of every row (and, in the last
+// level's launch, the padding rows); *operands_written reports whether it did (the
+// one-wavefront kernel of widths above 22 does not)
 bool launch_describe(const float* lvl, int B, int H, int W, int fw, int rotate, KpList kp,
                      int kcap, const int32_t* level_counts_all, int level, int L, double scale,
                      int32_t* out_xy, float* out_desc, float* out_conf, int64_t out_cap,
-                     int32_t* out_count, hipStream_t st);
+                     int32_t* out_count, const MatchOperands& mo, bool* operands_written, hipStream_t st);
 void launch_finalize_counts(const int32_t* level_counts_all, int B, int L, int32_t* out_count,
                             hipStream_t st);
 

@@ -35,13 +35,12 @@ constexpr int kNT = 64 * kWaves;       // threads per workgroup
 constexpr int kRowH = 128 + 8;         // padded fp16 row in LDS (272 B): conflict-free b128 reads
 constexpr int kCandCap = kMatchCandCap;  // admitted targets per query row (global list)
 constexpr int kHalfCap = kCandCap / 2;   // each half-wave's share of a row's list
-constexpr float kScale = 256.0f;       // operand pre-scale (2^8)
-constexpr float kLoScale = 2048.0f;    // lo part scale (2^11)
+constexpr float kScale = kMatchScale;      // operand pre-scale (2^8)
+constexpr float kLoScale = kMatchLoScale;  // lo part scale (2^11)
 
 // Per image: fp16 hi / lo (scaled) copies, squared norms (float32 of the float64 sum),
 // norms, and per-block maxima of both for the error bound (16 rows per workgroup, one wave
 // per row; the sweep reduces a pair's target-image maxima itself, so no extra launch).
-constexpr int kPrepRows = 16;
 __global__ void __launch_bounds__(256) k_match_prep(const float* __restrict__ desc,
                                                    const int32_t* __restrict__ count, int64_t cap,
                                                    int64_t capP, _Float16* __restrict__ hi,

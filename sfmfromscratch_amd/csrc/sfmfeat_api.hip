@@ -36,6 +36,10 @@ struct Level {
   double scale;
 };
 
+// slots beyond an extraction's batch the fused matcher operand buffers are sized for (a match
+// of the batch's table with a few extra slots then needs no reallocation)
+constexpr int kFusedPrepSpare = 8;
+
 }  // namespace
 
 // Lane gate (sfm_gate_*): the contexts of batches in flight share one; each extraction's
@@ -83,6 +87,13 @@ struct sfm_ctx {
   const int32_t* prep_count = nullptr;
   int prep_nimg = -1;
   int64_t prep_cap = -1;
+  // fused matcher operands (sfm_ctx_set_fused_prep): the last extraction on this context wrote
+  // the operands of slots [0, fp_B) of the table (fp_desc, fp_count, fp_cap) itself
+  bool fused_prep = false;
+  const float* fp_desc = nullptr;
+  const int32_t* fp_count = nullptr;
+  int64_t fp_cap = -1;
+  int fp_B = 0;
   bool match_direct = false;  // SFMFEAT_MATCH_DIRECT=1: all-pairs exact VALU kernel (A/B checks)
   bool exact_select = false;
   bool serial = false;        // SFMFEAT_SERIAL=1: no aux-stream overlap (diagnostic timings)
@@ -280,6 +291,22 @@ int skip_mask() {
   return m;
 }
 
+// The matcher operand buffers hold `nimg` slots of capP rows (no reallocation: false when they
+// are smaller, i.e. a prep of that many slots would reallocate them and lose their contents).
+bool match_operands_fit(const sfm_ctx* c, int nimg, int64_t capP) {
+  return c->m_hi.bytes >= (size_t)nimg * capP * 128 * 2 && c->m_imgmax.bytes >= (size_t)nimg * match_pmax_bytes(capP);
+}
+
+int match_operands_reserve(sfm_ctx* c, int nimg, int64_t capP) {
+  int rc;
+  if ((rc = ensure(c, c->m_hi, (size_t)nimg * capP * 128 * 2))) return rc;
+  if ((rc = ensure(c, c->m_lo, (size_t)nimg * capP * 128 * 2))) return rc;
+  if ((rc = ensure(c, c->m_norm2, (size_t)nimg * capP * 4))) return rc;
+  if ((rc = ensure(c, c->m_rnorm, (size_t)nimg * capP * 4))) return rc;
+  if ((rc = ensure(c, c->m_imgmax, (size_t)nimg * match_pmax_bytes(capP)))) return rc;
+  return SFM_OK;
+}
+
 int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy, float* desc,
                  float* conf, int32_t* count, int64_t cap, hipStream_t st) {
   if (B < 1 || H < 1 || W < 1) return set_err(c, SFM_EINVAL, "empty batch or image");
@@ -345,6 +372,22 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
     }
     if (!pyr_fused) pyramid_from(1);
   }
+  // fused matcher operands: buffers for the B slots (plus spare slots, so a match of the table
+  // with a few extra slots, e.g. BatchPipeline's halo slot, does not reallocate them), their
+  // per-block maxima zeroed ahead of the descriptor launches' atomic maxima
+  MatchOperands mo{nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+  c->fp_desc = nullptr;  // (a failed or non-fused extraction leaves no fused slots)
+  c->fp_B = 0;
+  if (c->fused_prep && !c->match_direct) {
+    const int64_t capP = (cap + 127) / 128 * 128;
+    if (!match_operands_fit(c, B + kFusedPrepSpare, capP) &&
+        (rc = match_operands_reserve(c, B + kFusedPrepSpare, capP)))
+      return rc;
+    mo = MatchOperands{as<_Float16>(c->m_hi), as<_Float16>(c->m_lo), as<float>(c->m_norm2), as<float>(c->m_rnorm),
+                       as<float2>(c->m_imgmax), capP};
+    HIPCHK(c, hipMemsetAsync(c->m_imgmax.p, 0, (size_t)B * match_pmax_bytes(capP), st));
+  }
+  bool fused_ok = mo.hi != nullptr;
   if (!zeroed || fill_launches) {
     HIPCHK(c, hipMemsetAsync(c->d_hist.p, 0, hist_bytes, st));
     HIPCHK(c, hipMemsetAsync(c->d_counts.p, 0, count_bytes, st));
@@ -423,11 +466,16 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   bool counted = false;  // the last level's describe launch wrote the slot counts
   auto describe_level = [&](int l, hipStream_t s) {
     StageScope sc(c, SFM_PROF_DESCRIBE, s);
-    if ((skip & 2) && l != L - 1) return;
+    if ((skip & 2) && l != L - 1) {
+      fused_ok = false;
+      return;
+    }
+    bool ow = false;
     const bool r = launch_describe(lvl[l], B, lv[l].h, lv[l].w, lv[l].fw, rotate, lb[l].kp, c->kcap,
                                    as<int32_t>(c->d_lc), l, L, lv[l].scale, xy, desc, conf, cap,
-                                   l == L - 1 ? count : nullptr, s);
+                                   l == L - 1 ? count : nullptr, mo, &ow, s);
     if (l == L - 1) counted = r;
+    fused_ok = fused_ok && ow;
   };
   // Harris launches: one per level, unless SFMFEAT_HARRIS_GROUP=g (g >= 1): levels >= g then
   // share launches (up to kHarrisMaxLevels each).  Off by default: grouping L1-L3 or L2-L3 cut
@@ -544,6 +592,12 @@ int extract_impl(sfm_ctx* c, const float* imgs, int B, int H, int W, int32_t* xy
   }
   if (!counted) launch_finalize_counts(as<int32_t>(c->d_lc), B, L, count, st);
   HIPCHK(c, hipGetLastError());
+  if (fused_ok && counted) {  // every level's descriptors (and the padding rows) carry operands
+    c->fp_desc = desc;
+    c->fp_count = count;
+    c->fp_cap = cap;
+    c->fp_B = B;
+  }
   return SFM_OK;
 }
 
@@ -568,11 +622,7 @@ int match_prep_range(sfm_ctx* c, const float* desc, const int32_t* count, int ni
     launch_transpose_desc(d0, count + lo, n, cap, capP, as<float>(c->m_descT) + (int64_t)lo * 128 * capP, st);
   } else {
     const int64_t capP = (cap + 127) / 128 * 128;
-    if ((rc = ensure(c, c->m_hi, (size_t)nimg * capP * 128 * 2))) return rc;
-    if ((rc = ensure(c, c->m_lo, (size_t)nimg * capP * 128 * 2))) return rc;
-    if ((rc = ensure(c, c->m_norm2, (size_t)nimg * capP * 4))) return rc;
-    if ((rc = ensure(c, c->m_rnorm, (size_t)nimg * capP * 4))) return rc;
-    if ((rc = ensure(c, c->m_imgmax, (size_t)nimg * match_pmax_bytes(capP)))) return rc;
+    if ((rc = match_operands_reserve(c, nimg, capP))) return rc;
     if (n == 0) return SFM_OK;
     StageScope sc(c, SFM_PROF_MATCH_PREP, st);
     const int64_t o = (int64_t)lo * capP;
@@ -592,7 +642,13 @@ int match_impl(sfm_ctx* c, const float* desc, const int32_t* count, int nimg, in
     return set_err(c, SFM_EINVAL, "match capacity must be in [1, 16384]");
   int rc;
   if (prep) {
-    if ((rc = match_prep_range(c, desc, count, nimg, cap, 0, nimg, st))) return rc;
+    // slots the last extraction on this context wrote with their operands (fused prep) keep
+    // them; only the rest of the table is prepped (none in BatchPipeline's own tables)
+    int lo = 0;
+    if (!c->match_direct && c->fp_desc == desc && c->fp_count == count && c->fp_cap == cap && c->fp_B <= nimg &&
+        match_operands_fit(c, nimg, (cap + 127) / 128 * 128))
+      lo = c->fp_B;
+    if ((rc = match_prep_range(c, desc, count, nimg, cap, lo, nimg - lo, st))) return rc;
   } else {  // operands from earlier sfm_match_prep_dev calls on this same table
     // (which slots the device-resident pairs touch, and whether their descriptors changed
     // since, cannot be checked without a host sync: that part is the caller's contract)
@@ -1136,6 +1192,14 @@ int32_t sfm_match(sfm_ctx* c, const float* d1, int64_t n1, const float* d2, int6
     if (matches)
       for (int64_t i = 0; i < 2 * k; ++i) matches[i] = mm[i];
   }
+  return SFM_OK;
+}
+
+int32_t sfm_ctx_set_fused_prep(sfm_ctx* c, int32_t on) {
+  if (!c) return SFM_EINVAL;
+  c->fused_prep = on != 0;
+  c->fp_desc = nullptr;
+  c->fp_B = 0;
   return SFM_OK;
 }
 

@@ -174,6 +174,12 @@ class BatchPipeline:
             serial_lanes = [int(v) for v in env.replace("+", ",").split(",") if v.strip()]
         self.lane_streams = lane_streams
         self.serial_lanes = sorted(set(int(v) for v in serial_lanes))
+        # fused matcher operands (sfm_ctx_set_fused_prep): each lane's extraction writes the
+        # matcher's operands of its batch, so the match launches no operand prep for them (its
+        # table is the lane's own; the halo hook writes only the extra slots, which the match
+        # preps).  SFMFEAT_FUSED_PREP=0: the separate prep launch (A/B)
+        fused_prep = os.environ.get("SFMFEAT_FUSED_PREP", "1") != "0"
+        self.fused_prep = fused_prep
         self.B, self.H, self.W = batch, H, W
         self.inflight = max(1, int(inflight))
         self.pairs = pairs
@@ -185,6 +191,8 @@ class BatchPipeline:
             ex.reserve(batch, H, W)
             if li in self.serial_lanes:
                 ex.ctx.set_serial(True)
+            if fused_prep:
+                ex.ctx.set_fused_prep(True)
             if lane_streams == "context":
                 if li == 0 and lane_prio:
                     ex.ctx.set_priority(-1)
@@ -203,6 +211,8 @@ class BatchPipeline:
                     torch.zeros((max(P, 1),), dtype=torch.int32, device=dev))
             self.lanes.append({"ex": ex, "m": m, "slots": slots, "view": view, "mout": mout, "stream": stream})
         self.cap = self.lanes[0]["ex"].cap
+        # pairs within the batch only (no halo pair): the match reads the batch's slots alone
+        self.batch_only_pairs = P == 0 or int(pairs.max().item()) < batch
         self.n = 0
         self.gate = None
         if gate and self.inflight > 1:
@@ -240,7 +250,7 @@ class BatchPipeline:
                 ln["hold_ev"].record(ln["stream"])
             if hook is not None:
                 hook(ln["slots"], self.B)
-            ln["m"].match(ln["slots"], self.pairs, out=ln["mout"])
+            ln["m"].match(ln["view"] if self.batch_only_pairs else ln["slots"], self.pairs, out=ln["mout"])
         return ln
 
     def join(self):

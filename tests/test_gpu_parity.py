@@ -344,6 +344,48 @@ def test_pipeline_batches_in_flight_match_serial(gate, lane_streams, serial_lane
             assert torch.equal(mm[p, :k], ln["mout"][0][p, :k]) and torch.equal(mc[p, :k], ln["mout"][1][p, :k])
 
 
+def test_pipeline_fused_matcher_operands_1080p_with_halo_vs_oracle():
+    """BatchPipeline's lanes extract with fused matcher operands (sfm_ctx_set_fused_prep: the
+    descriptor kernel writes the split-f16 operands, norms and block maxima of every row, and
+    the last level's launch the padding rows), so the match preps only the halo slot the hook
+    filled.  At 1080p P-oct with the halo pair (B-1, B): keypoints, descriptors and every pair's
+    matches equal the oracle's."""
+    torch = pytest.importorskip("torch")
+    from sfmfromscratch_amd import distributed as D
+    from sfmfromscratch_amd.pipeline import BatchPipeline
+    B, H, W = 4, 1080, 1920
+    frames = [synth.make_frame(H, W, 77, i) for i in range(B)]
+    pairs_np = D.local_consecutive_pairs(B, 0, 2)  # (0,1) .. (B-2,B-1), (B-1, B)
+    pipe = BatchPipeline(P_OCT, 0.85, B, H, W, torch.from_numpy(pairs_np).cuda(), inflight=2, extra_slots=1)
+    assert pipe.fused_prep and not pipe.batch_only_pairs
+
+    def halo(slots, n):  # slot B := slot 0 (what a neighbour rank's first frame would be)
+        slots.xy[n].copy_(slots.xy[0])
+        slots.desc[n].copy_(slots.desc[0])
+        slots.count[n:n + 1].copy_(slots.count[0:1])
+
+    batch = torch.from_numpy(np.stack(frames)).cuda()
+    for _ in range(2):  # both lanes
+        ln = pipe.submit(batch, hook=halo)
+    pipe.join()
+    torch.cuda.synchronize()
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(B) as pool:
+        ext = list(pool.map(lambda f: O.extract(f, P_OCT), frames))
+    descs = [e[2] for e in ext] + [ext[0][2]]
+    counts = ln["slots"].count.cpu().numpy()
+    for i, (OX, OY, OD, _) in enumerate(ext):
+        n = int(counts[i])
+        assert n == len(OX)
+        assert np.array_equal(bits(ln["slots"].desc[i, :n].cpu().numpy()), bits(OD))
+    mm, mc, nm = (t.cpu().numpy() for t in ln["mout"])
+    for p, (i, j) in enumerate(pairs_np):
+        om, oc = O.match(descs[i], descs[j], 0.85)
+        k = int(nm[p])
+        assert k == len(oc), (i, j)
+        assert_matches_equal(om, oc, mm[p, :k], mc[p, :k])
+
+
 P_4K = dict(P_MAIN, num_interest_points=8000, pyramid_level=5, pyramid_scale_factor=2)
 
 
