@@ -297,7 +297,7 @@ def main():
     ap.add_argument("--emulate-exchange", type=int, default=0, metavar="WG",
                     help="c4 at one GPU: a single-GPU rehearsal of one rank of an --emulate-world-rank job: after "
                          "each chunk's extraction a WG-workgroup device copy of the bytes that rank would receive "
-                         "(count-compacted all-gather) on a high-priority stream, the chunk's pairs waiting for it; "
+                         "(count-compacted all-gather) on a high-priority stream beside the extraction; "
                          "reports the extraction slowdown and the hidden fraction of the emulated exchange")
     ap.add_argument("--emulate-world", type=int, default=8)
     ap.add_argument("--verify", action="store_true",
@@ -998,8 +998,9 @@ def run_emulated_exchange(args, torch, dev, D, plan, frames, timed, n_global):
     rank of an N-rank run (--frames = its shard, e.g. 256 = 2,048 / 8), first alone (T_compute),
     then with an emulated exchange per chunk (T_emu): a WG-workgroup copy of the bytes the rank
     would receive — (N - 1) x 32 frames x (M rows x 520 B + 4), M the largest keypoint count —
-    on a high-priority stream, the chunk's pairs waiting for it (distributed.ChunkedGatherJob
-    `emulate`).  hidden_fraction = 1 - (T_emu - T_compute) / T_copies_alone.  It measures the
+    on a high-priority stream beside the extraction; the rank's own pairs do not wait for it, as
+    in the multi-rank job (distributed.ChunkedGatherJob `emulate`); the job ends after the last
+    copy.  hidden_fraction = 1 - (T_emu - T_compute) / T_copies_alone.  It measures the
     collective's CU and HBM contention with extraction, not xGMI latency."""
     job = D.ChunkedGatherJob(P_OCT, RATIO, plan, 0, H, W, inflight=args.inflight, device=dev.index)
     for _ in range(max(1, args.warmup)):
@@ -1019,7 +1020,8 @@ def run_emulated_exchange(args, torch, dev, D, plan, frames, timed, n_global):
     e = ejob.emulate
     comm = {"kind": (f"EMULATED exchange on one GPU: per chunk a {e['workgroups']}-workgroup device copy of the "
                      f"{e['bytes_per_chunk']} B one rank of a {e['world']}-rank job receives (count-compacted rows, "
-                     f"M = {rows}) on a high-priority stream; the chunk's pairs wait for it"),
+                     f"M = {rows}) on a high-priority stream beside the extraction; the rank's own pairs do not "
+                     "wait for it, the job ends after the last copy"),
             "emulated_world": e["world"], "workgroups": e["workgroups"], "rows": rows,
             "bytes_per_chunk": e["bytes_per_chunk"], "chunks": plan.C,
             "copies_alone_ms": round(t_alone * 1e3, 3),

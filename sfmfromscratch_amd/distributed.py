@@ -264,7 +264,7 @@ def allgather_chunk_counts(dist, table, plan: GatherPlan, c: int, src, async_op:
 
 
 def allgather_chunk_rows(dist, table, plan: GatherPlan, c: int, src, stage: CompactStage, M: int,
-                         group=None, coalesce: bool = False):
+                         group=None, coalesce: bool = False, skip_rank: int | None = None):
     """Phase 2: the first M rows (M = the chunk's largest count over every rank, read on the
     host after phase 1) of every slot's desc and xy — the rows a count-aware reader (the
     matcher's prep, the checksums) ever reads — packed per rank, gathered and unpacked into
@@ -290,8 +290,14 @@ def allgather_chunk_rows(dist, table, plan: GatherPlan, c: int, src, stage: Comp
                  dist.all_gather_into_tensor(rx, sx.view(-1), group=group, async_op=True)]
     for w in works:  # the unpack waits for the gather on the current stream (RCCL: no host wait)
         w.wait()
-    table.desc[base:base + n, :M].copy_(rd.view(n, M, 128))
-    table.xy[base:base + n, :M].copy_(rx.view(n, M, 2))
+    rdv, rxv = rd.view(n, M, 128), rx.view(n, M, 2)
+    # skip_rank: the rank whose rows `src` already holds in the table (the caller's own slots,
+    # read by its matcher meanwhile) are not rewritten
+    spans = [(0, n)] if skip_rank is None else [(0, skip_rank * bc), ((skip_rank + 1) * bc, n)]
+    for a, e in spans:
+        if e > a:
+            table.desc[base + a:base + e, :M].copy_(rdv[a:e])
+            table.xy[base + a:base + e, :M].copy_(rxv[a:e])
     return works, (plan.world - 1) * bc * M * (128 * 4 + 2 * 4)
 
 
@@ -395,8 +401,12 @@ class ChunkedGatherJob:
                 rp = plan.rank_pairs(rank)
                 self.sched = plan.schedule(rp)
                 self.rank_pairs_n = len(rp)
+        # world > 1 (all-gather): each chunk is extracted straight into this rank's slots of the
+        # chunk's table region, which are also the collective's send buffer (in place), so the
+        # pairs of two own frames are matched right after the extraction and only the pairs
+        # with another rank's frame wait for the gather (consecutive pairs: one per rank)
         for ln in self.lanes:
-            ln["slots"] = SlotTable(torch, Bx, cap, dev) if world > 1 and not self.halo else None
+            ln["slots"] = None
         # count-compacted gather (default on for the multi-rank all-gather; SFM_GATHER_COMPACT=0
         # gathers full-capacity slots): counts first, then only each chunk's first M rows
         if compact is None:
@@ -412,7 +422,18 @@ class ChunkedGatherJob:
         self.gathered_rows = []  # per chunk of the last run: M (compact) or cap
         self.CH = 4096  # 'all': pairs per matcher launch
         self.keep_all_results = bool(keep_all_results)
+        self.n_local = None
         if self.sched is not None:
+            if world > 1 and not self.halo:
+                # per chunk: the pairs of two own frames first (n_local[c] of them), then the rest
+                own = np.zeros(plan.n, bool)
+                own[plan.slot_of(np.arange(rank * S, rank * S + S))] = True
+                srt, nl = [], []
+                for p in self.sched:
+                    loc = own[p[:, 0]] & own[p[:, 1]] if len(p) else np.zeros(0, bool)
+                    srt.append(np.concatenate([p[loc], p[~loc]]).reshape(-1, 2).astype(np.int32))
+                    nl.append(int(loc.sum()))
+                self.sched, self.n_local = srt, nl
             self.sched_dev = [torch.from_numpy(np.ascontiguousarray(p, np.int32)).to(dev) for p in self.sched]
             self.outs = [self._new_out(len(p)) for p in self.sched]
         else:
@@ -425,9 +446,11 @@ class ChunkedGatherJob:
         # chunk's extraction, a copy of the bytes one rank of an `emulate["world"]`-rank job
         # receives for that chunk — (world - 1) x chunk frames x (rows x 520 B + 4), the
         # count-compacted all-gather's payload — on a high-priority stream by
-        # `emulate["workgroups"]` persistent workgroups (a collective kernel's launch shape), and
-        # the chunk's pairs wait for it as they wait for the real gather.  It reproduces the
-        # collective's CU residency and local HBM traffic beside extraction, not xGMI latency.
+        # `emulate["workgroups"]` persistent workgroups (a collective kernel's launch shape); the
+        # chunk's pairs, all of two own frames at world 1 like every consecutive pair but one
+        # per rank in the real job, do not wait for it, and the job ends after the last copy.
+        # It reproduces the collective's CU residency and local HBM traffic beside extraction,
+        # not xGMI latency.
         self.emulate = None
         if emulate:
             if world != 1:
@@ -484,9 +507,32 @@ class ChunkedGatherJob:
         compact = self.compact and exchange
         waiting = []  # compact: chunks whose counts are in flight, (c, lane, count works)
 
+        gathered = world > 1 and not self.halo  # the all-gather (own slots extracted in place)
+
+        def match_pairs(c, lo, hi):
+            k = hi - lo
+            if k > 0:
+                o = self.outs[c]
+                self.matcher.match(self.table, self.sched_dev[c][lo:hi], out=(o[0][lo:hi], o[1][lo:hi], o[2][lo:hi]),
+                                   prepped=True)
+
+        def match_local(c, ln):
+            """All-gather jobs: chunk c's own slots get their matcher operands and the pairs of
+            two own frames ready with chunk c are matched, after the lane's extraction — not
+            after the collective."""
+            if self.sched is None:
+                return
+            bc, base = plan.chunk_size(c), plan.chunk_base(c)
+            with torch.cuda.stream(self.mstream):
+                self.mstream.wait_stream(ln["stream"])
+                self.matcher.prep(self.table, base + rank * bc, bc)
+                match_pairs(c, 0, self.n_local[c])
+
         def match_chunk(c, works, ln, ready=None):
             """Prep chunk c's slots and match its ready pairs on the matcher stream, after the
-            chunk's collectives (`works`), its unpack (`ready` event) or its lane."""
+            chunk's collectives (`works`), its unpack (`ready` event) or its lane (all-gather
+            jobs: the other ranks' slots of the chunk and the pairs with another rank's frame;
+            match_local did the own ones)."""
             if self.sched is None:
                 return
             bc, l0 = plan.chunk_size(c), c * Bx
@@ -505,9 +551,15 @@ class ChunkedGatherJob:
                 # chunks' slots reuse theirs
                 if self.halo:
                     self.matcher.prep(self.table, l0, bc + (1 if c == C - 1 and world > 1 else 0))
+                elif gathered:
+                    base = plan.chunk_base(c)
+                    self.matcher.prep(self.table, base, rank * bc)
+                    self.matcher.prep(self.table, base + (rank + 1) * bc, (world - rank - 1) * bc)
                 else:
                     self.matcher.prep(self.table, plan.chunk_base(c), world * bc)
-                if len(self.sched[c]):
+                if gathered:
+                    match_pairs(c, self.n_local[c], len(self.sched[c]))
+                elif len(self.sched[c]):
                     self.matcher.match(self.table, self.sched_dev[c], out=self.outs[c], prepped=True)
 
         def finish_compact(c, ln, cworks):
@@ -518,8 +570,9 @@ class ChunkedGatherJob:
                 for w in cworks:
                     w.wait()
                 M = int(self.table.count[base:base + world * bc].max().item()) if bc else 0
-                works, _ = allgather_chunk_rows(dist, self.table, plan, c, ln["slots"], ln["stage"], M,
-                                                group=self.group, coalesce=self.coalesce)
+                own = self._view(self.table, base + rank * bc, bc)
+                works, _ = allgather_chunk_rows(dist, self.table, plan, c, own, ln["stage"], M,
+                                                group=self.group, coalesce=self.coalesce, skip_rank=rank)
                 ln["pending"] = works
                 done = torch.cuda.Event()
                 done.record(ln["stream"])  # the unpacked rows are in the table
@@ -543,19 +596,23 @@ class ChunkedGatherJob:
                 elif world == 1:
                     ln["ex"].extract(frames[l0:l0 + bc], out=self._view(self.table, plan.chunk_base(c), bc))
                     if self.emulate is not None and exchange:
-                        ready = self._emulated_gather(ln["stream"])
-                        match_chunk(c, None, ln, ready=ready)
-                        continue
+                        # the rank's own pairs do not wait for its gather (as in the multi-rank
+                        # job): the copy only competes for CUs and HBM; the job ends after it
+                        self._emulated_gather(ln["stream"])
                 else:
-                    ln["ex"].extract(frames[l0:l0 + bc], out=self._view(ln["slots"], 0, bc))
+                    # this rank's slots of the chunk's table region: extraction output, the
+                    # matcher's input for the own pairs, and the collective's send buffer
+                    own = self._view(self.table, plan.chunk_base(c) + rank * bc, bc)
+                    ln["ex"].extract(frames[l0:l0 + bc], out=own)
+                    match_local(c, ln)
                     if record_sent:
                         g0 = plan.local_frames(rank, c)[0]
-                        self.sent_ck[g0:g0 + bc] = slot_checksums(torch, self._view(ln["slots"], 0, bc))
+                        self.sent_ck[g0:g0 + bc] = slot_checksums(torch, own)
                     if compact:
-                        cworks = allgather_chunk_counts(dist, self.table, plan, c, ln["slots"], async_op=True,
+                        cworks = allgather_chunk_counts(dist, self.table, plan, c, own, async_op=True,
                                                         group=self.group)
                     elif exchange:
-                        works = self.gather_chunk(c, ln["slots"])
+                        works = self.gather_chunk(c, own)
                         ln["pending"] = works
                         self.gathered_rows.append(self.cap)
             if compact:
@@ -574,6 +631,8 @@ class ChunkedGatherJob:
                     w.wait()
                 ln["pending"] = None
         cur.wait_stream(self.mstream)
+        if self.emulate is not None and exchange:
+            cur.wait_stream(self.emulate["stream"])
         if self.sched is None:  # 'all': deal by cost once the counts are gathered (host sync)
             counts = self.table.count.cpu().numpy()
             mine = weighted_deal(self.all_pairs, counts[plan.slot_of(np.arange(plan.n))], world)[rank]
@@ -634,19 +693,20 @@ class ChunkedGatherJob:
         each chunk's M, rows, unpack; else full-capacity slots), on lane 0's last slots."""
         import time
         torch, dist, plan = self.torch, self.dist, self.plan
-        src, stage = self.lanes[0]["slots"], self.lanes[0]["stage"]
+        stage = self.lanes[0]["stage"]
         dist.barrier(group=self.group)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
             for c in range(plan.C):
+                src = self._view(self.table, plan.chunk_base(c) + self.rank * plan.chunk_size(c), plan.chunk_size(c))
                 if self.compact:
                     for w in allgather_chunk_counts(dist, self.table, plan, c, src, async_op=True, group=self.group):
                         w.wait()
                     bc, base = plan.chunk_size(c), plan.chunk_base(c)
                     M = int(self.table.count[base:base + plan.world * bc].max().item())
                     allgather_chunk_rows(dist, self.table, plan, c, src, stage, M, group=self.group,
-                                         coalesce=self.coalesce)
+                                         coalesce=self.coalesce, skip_rank=self.rank)
                 else:
                     for w in self.gather_chunk(c, src):
                         w.wait()

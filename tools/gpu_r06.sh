@@ -44,6 +44,12 @@ for s in ${STEPS:-tests smoke bench trace}; do
         python -c "import json;d=json.load(open('$O/${T}_bench_c4.out'));print('c4', d['value'], d['ms_per_step'], d.get('collective'))" ;;
     c5) step bench_c5 300 python bench.py --workload c5 --steps 100 --warmup 5 --cpu-sample 0
         python -c "import json;d=json.load(open('$O/${T}_bench_c5.out'));print('c5', d['value'], d['ms_per_step'])" ;;
+    emu)
+      step emu_bench 300 python bench.py --workload c4 --frames 256 --steps 5 --warmup 2 --emulate-exchange ${EMU_WG:-32}
+      python -c "import json;d=json.load(open('$O/${T}_emu_bench.out'));print('emu', json.dumps(d['collective']))"
+      step emu_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_emu_prof -o run -- python bench.py --workload c4 --frames 256 --steps 2 --warmup 1 --emulate-exchange ${EMU_WG:-32}
+      python tools/trace_summary.py $O/${T}_emu_prof > $O/${T}_emu_trace_summary.txt
+      python tools/trace_gantt.py $O/${T}_emu_prof 3 2 k_copy_wg > $O/${T}_emu_gantt.txt || true ;;
     sq)
       step pmc_sq 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d $O/${T}_pmc_sq -o run -- python bench.py --steps 2 --warmup 1 --cpu-sample 0 --no-profile
       python tools/sq_summary.py $O/${T}_pmc_sq $O/${T}_sq_counters "# $T build, bench.py --steps 2 --warmup 1" > /dev/null ;;
