@@ -31,6 +31,14 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 constexpr int kHT = 64;   // output tile columns (rows: HarrisShape::TH, 64 or 32)
+// SFM_HARRIS_COUNT_INTERIOR (instruction counting only, tools/isa_phases.py --interior; never
+// run): every tile takes the interior-tile code path, so the static count of the tile loop is
+// the per-tile-wave count of the tiles that lie inside the image (all but the border tiles)
+#ifdef SFM_HARRIS_COUNT_INTERIOR
+#define SFM_INTERIOR(cond) true
+#else
+#define SFM_INTERIOR(cond) (cond)
+#endif
 // levels with at most this many 64 x 64 tiles per resident workgroup take the 64 x 32 form
 // (SFMFEAT_HARRIS_SMALL overrides; 0 = never)
 constexpr int kHarrisSmallTiles = 4;
@@ -287,7 +295,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     const int gx0 = (tile % tiles_x) * kHT - XA;
     const int gy0 = (tile / tiles_x) * TH - GA - 1;
     okmask = 0;
-    if (VEC && gx0 >= 0 && gx0 + IWP <= W && gy0 >= 0 && gy0 + IH <= H) {
+    if (VEC && SFM_INTERIOR(gx0 >= 0 && gx0 + IWP <= W && gy0 >= 0 && gy0 + IH <= H)) {
       const float* tb = img + (int64_t)gy0 * W + gx0;
 #pragma unroll
       for (int k = 0; k < NIMG; ++k) t4[VEC ? k : 0] = *reinterpret_cast<const f32x4*>(tb + (VEC ? eoff[k] : 0));
@@ -339,7 +347,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
     if constexpr (ABL != 4) __syncthreads();  // the previous tile's LDS reads are done
     // 0. the prefetched image tile -> LDS, then start fetching the next tile (a tile whose
     //    whole image window lies inside the image stores its loads unmasked)
-    const bool img_in = tx0 - XA >= 0 && tx0 - XA + IWP <= W && ty0 - GA - 1 >= 0 && ty0 - GA - 1 + IH <= H;
+    const bool img_in = SFM_INTERIOR(tx0 - XA >= 0 && tx0 - XA + IWP <= W && ty0 - GA - 1 >= 0 && ty0 - GA - 1 + IH <= H);
     if (VEC && img_in) {
 #pragma unroll
       for (int k = 0; k < NIMG; ++k) {
@@ -461,7 +469,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
       }
     };
     // every gradient position of the tile (incl. the unused stride padding) in the image
-    const bool grad_in = tx0 - GA >= 0 && tx0 - GA + PWP <= W && ty0 - GA >= 0 && ty0 - GA + PH <= H;
+    const bool grad_in = SFM_INTERIOR(tx0 - GA >= 0 && tx0 - GA + PWP <= W && ty0 - GA >= 0 && ty0 - GA + PH <= H);
     if (grad_in) sobel(std::false_type{});
     else sobel(std::true_type{});
     if constexpr (ABL != 4) __syncthreads();
@@ -472,7 +480,11 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
       // After the Sobel barrier, so the other waves start their windows meanwhile (form 0
       // keeps the image tile intact until the next tile's copy)
       float* const d1 = lvs.l[li].down[0];
+#ifdef SFM_HARRIS_COUNT_NO_DOWN  // instruction counting only (tools/isa_phases.py --interior)
+      if (false) {
+#else
       if (d1 != nullptr && tid < 64) {
+#endif
         const int bx = tid & 7, by = tid >> 3;
         const int gy = ty0 + 8 * by, gx = tx0 + 8 * bx;
         if (gy < H && gx < W) {
@@ -718,7 +730,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
         for (int q = 0; q < 4; ++q) {
           Rq[q] = Rpk[o >> 1][q][o & 1];
           if (ABL != 1)
-            atomicAdd(&s_hc[fkey(Rq[q]) >> (32 - kMedBits1)], (FULL || (gy < H && gx0 + q < W)) ? 1u : 0u);
+            atomicAdd(&s_hc[fkey_nz(Rq[q]) >> (32 - kMedBits1)], (FULL || (gy < H && gx0 + q < W)) ? 1u : 0u);
         }
         if (FULL || gy < H) {
           float* dst = Rp + (int64_t)gy * W + gx0;
@@ -732,7 +744,7 @@ __global__ void __launch_bounds__(HarrisShape<F>::NT, HarrisShape<F>::WPE) k_har
         }
       }
     };
-    if (ty0 + TH <= H && tx0 + kHT <= W) epilogue(std::true_type{});
+    if (SFM_INTERIOR(ty0 + TH <= H && tx0 + kHT <= W)) epilogue(std::true_type{});
     else epilogue(std::false_type{});
     }  // !MF
     if constexpr (ABL == 3) {

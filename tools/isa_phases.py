@@ -15,7 +15,12 @@ The tile loop runs from its first s_barrier to the backward branch that closes i
             every wave ran it: an upper bound)
 The phases are classified by opcode (the compiler interleaves R and the histogram with the
 window's last rows), so the table is per tile-wave, not a timeline.
-usage: tools/isa_phases.py [lib.so] [kernel-substring]"""
+With --interior the tool compiles harris.hip itself with -DSFM_HARRIS_COUNT_INTERIOR (every
+tile takes the interior-tile path: unmasked prefetch, tile copy, Sobel and epilogue), so the
+static count of the tile loop is exactly the VALU count per tile-wave of an interior tile — the
+tiles that do not touch the image border (all but 92 of the 510 per 1080p plane).  Without it
+the loop holds both variants of each masked phase and the count is an upper bound.
+usage: tools/isa_phases.py [--interior] [lib.so] [kernel-substring]"""
 import collections
 import os
 import re
@@ -73,10 +78,21 @@ def branch_target(ins, k):
     return None
 
 
-def main():
-    lib = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "sfmfromscratch_amd", "lib", "libsfmfeat.so")
-    pat = sys.argv[2] if len(sys.argv) > 2 else "k_harrisILi7ELb1ELi0ELi0E"
-    name, ins = kernel_body(disassemble(lib), pat)
+def interior_object(tmp, no_down=False):
+    """harris.hip compiled with every tile on the interior path (the product flags + the macro);
+    no_down: also without the fused pyramid block (run by the first wave only)."""
+    src = os.path.join(ROOT, "sfmfromscratch_amd", "csrc", "harris.hip")
+    out = os.path.join(tmp, "harris_interior%s.o" % ("_nd" if no_down else ""))
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+                    "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize",
+                    "-DSFM_HARRIS_COUNT_INTERIOR"] + (["-DSFM_HARRIS_COUNT_NO_DOWN"] if no_down else []) +
+                   ["-c", src, "-o", out], check=True, stderr=subprocess.DEVNULL)
+    return out
+
+
+def phase_counts(ins):
+    """(counter by phase, tile-loop bounds, barriers, Sobel loops, window pk / scalar fmas) of
+    one kernel body."""
     # the tile loop: the backward branch with the largest span
     loop = None
     for k, (op, args, _) in enumerate(ins):
@@ -98,7 +114,7 @@ def main():
     NT, PH, NS = 256, 70, 18
     trips = -(-PH * NS // NT)
     cnt = collections.Counter()
-    hist_ops = {"v_not_b32_e32", "v_lshrrev_b32_e32", "v_and_b32_e32"}
+    hist_ops = {"v_not_b32_e32", "v_lshrrev_b32_e32", "v_and_b32_e32", "v_xor3_b32", "v_ashrrev_i32_e32"}
     for k in range(a, b + 1):
         op = ins[k][0]
         if not op.startswith("v_") and not op.startswith("ds_add"):
@@ -113,23 +129,48 @@ def main():
             cnt["window fmas"] += 1
         elif op == "v_pk_mul_f32":
             cnt["products"] += 1
-        elif op in ("v_mul_f32_e32", "v_sub_f32_e32", "v_add_f32_e32"):
+        elif op == "v_pk_add_f32":
             cnt["R (det - alpha tr^2)"] += 1
+        elif op in ("v_mul_f32_e32", "v_sub_f32_e32", "v_add_f32_e32"):
+            cnt["scalar f32 (R / fused pyramid)"] += 1
         elif op in hist_ops or op.startswith("ds_add"):
             cnt["histogram key + LDS add"] += 1
         elif op.startswith(("v_cmp", "v_cndmask")):
             cnt["masks (tile copy, hist bounds)"] += 1
         else:
             cnt["addressing / moves"] += 1
+    win = sum(1 for k in range(a, b + 1) if ins[k][0] == "v_pk_fma_f32" and not any(t <= k <= e for t, e in inner))
+    sc = sum(1 for k in range(a, b + 1) if ins[k][0] in ("v_fmac_f32_e32", "v_fma_f32"))
+    return cnt, (a, b), bars, inner, trips, win, sc
+
+
+def main():
+    args = [a for a in sys.argv[1:] if a != "--interior"]
+    interior = "--interior" in sys.argv[1:]
+    pat = args[1] if len(args) > 1 else "k_harrisILi7ELb1ELi0ELi0E"
+    if interior:
+        tmpd = tempfile.TemporaryDirectory()
+        name, ins = kernel_body(disassemble(interior_object(tmpd.name)), pat)
+        _, ins_nd = kernel_body(disassemble(interior_object(tmpd.name, no_down=True)), pat)
+    else:
+        lib = args[0] if args else os.path.join(ROOT, "sfmfromscratch_amd", "lib", "libsfmfeat.so")
+        name, ins = kernel_body(disassemble(lib), pat)
+    cnt, (a, b), bars, inner, trips, win, sc = phase_counts(ins)
+    if interior:
+        # the fused pyramid block runs in the first wave of the four only: its instructions (the
+        # difference to the build without it) count 1/4 per tile-wave
+        cnt_nd = phase_counts(ins_nd)[0]
+        down = collections.Counter({k: cnt[k] - cnt_nd.get(k, 0) for k in cnt})
+        cnt = collections.Counter({k: cnt_nd.get(k, 0) + down[k] / 4.0 for k in cnt})
+        print(f"(interior tiles; the fused-pyramid block, {sum(down.values())} VALU in wave 0 only, counted 1/4)")
     tot = sum(cnt.values())
     print(f"{name}: tile loop {b - a + 1} instructions, {len(bars)} barriers, sobel loops {len(inner)} "
           f"(trip count {trips})")
-    print(f"{'phase':22s} {'VALU/tile-wave':>14s} {'share':>7s}")
+    print(f"{'phase':30s} {'VALU/tile-wave':>14s} {'share':>7s}")
     for k, v in sorted(cnt.items(), key=lambda kv: -kv[1]):
-        print(f"{k:22s} {v:14.0f} {v / tot:7.1%}")
-    print(f"{'total':22s} {tot:14.0f}")
-    win = sum(1 for k in range(a, b + 1) if ins[k][0] == "v_pk_fma_f32" and not any(t <= k <= e for t, e in inner))
-    sc = sum(1 for k in range(a, b + 1) if ins[k][0] in ("v_fmac_f32_e32", "v_fma_f32"))
+        print(f"{k:30s} {v:14.1f} {v / tot:7.1%}")
+    print(f"{'total':30s} {tot:14.1f}")
+    print(f"{'non-window':30s} {tot - cnt['window fmas']:14.1f}")
     print(f"window: {win} v_pk_fma_f32 + {sc} scalar fmas = {2 * win + sc} fmas "
           f"(16 px x 147 = 2352 per tile-thread)")
 
