@@ -75,13 +75,13 @@ SFM_DEV uint32_t fkey(float v) {
   if (b == 0x80000000u) b = 0u;
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
-// fkey for values that are never -0 (two VALU ops: an arithmetic shift and a three-way xor):
-// for b >= 0, b ^ 0x80000000 = b | 0x80000000; for b < 0, b ^ 0xffffffff = ~b.  Harris's R is
-// never -0 (det = t1 - t2 of non-negative products, at = alpha tr^2 >= +0, and x - x = +0), so
-// its digit-1 histogram takes this form (tests/test_gpu_parity.py pins the R map and median).
+// fkey for values that are never -0 (three VALU ops, no compare): b ^ m with m = 0x80000000
+// for b >= 0 (b | 0x80000000) and m = 0xffffffff for b < 0 (~b).  Harris's R is never -0
+// (det = t1 - t2 of non-negative products, at = alpha tr^2 >= +0, and x - x = +0), so its
+// digit-1 histogram takes this form (tests/test_gpu_parity.py pins the R map and median).
 SFM_DEV uint32_t fkey_nz(float v) {
   const uint32_t b = __float_as_uint(v);
-  return b ^ (uint32_t)((int32_t)b >> 31) ^ 0x80000000u;
+  return b ^ ((uint32_t)((int32_t)b >> 31) | 0x80000000u);
 }
 SFM_DEV float fkey_inv(uint32_t k) {
   uint32_t b = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;

@@ -22,8 +22,8 @@
 
 namespace sfm {
 
-constexpr int kTieLdsCap = 4096;
 constexpr int kTopkDirect = 2048;  // candidates sorted whole; above: radix select first
+constexpr int kTieLdsCap = 2048;   // confidence ties of the k-th key sorted in LDS; more: radix in global
 
 // LDS histogram add (pred lanes add 1 to h[bin]); agg: the lanes on the first active lane's
 // bin fold into one add by that lane (planes where many keys share a bin, e.g. R == 0 runs,
@@ -115,13 +115,20 @@ SFM_DEV uint32_t radix_select_regs(const uint64_t (&kr)[R], int64_t m, uint32_t*
 
 constexpr int kRegKeys = 8;  // keys per thread held in registers by the top-k (C <= 8192)
 
+// The workgroup's LDS is sized per launch from k (select_sel_cap): a bitonic sort of n > 2048
+// keys runs over next_pow2(n) slots, so the sel area holds max(next_pow2(k), kTopkDirect) keys
+// (4096 at k = 2500: 68 KB in all, against 100 KB for the largest k), and a select workgroup
+// fits on a CU beside one k_harris workgroup (78.8 KB).  Its VGPRs are kept at <= 88 for the
+// same reason: 4 waves per SIMD x 88 + one k_harris wave (160) = 512, the SIMD's register file
+// (tests/test_isa_guard_cpu.py pins both budgets).
 struct SelectLds {
-  uint64_t* sel;   // kTopkLdsCap
+  uint64_t* sel;   // sel_cap
   uint64_t* tie;   // kTieLdsCap
   uint32_t* h;     // kHistBins
   uint32_t* scan;  // 1024
   uint32_t* out;   // 2
   uint32_t* cnt;   // 2
+  int med_cap;     // u32 median-list keys held over the sel + tie areas
 };
 
 // The kk (>= 1) smallest of the C keys cp[0..C) into L.sel[0..kk), ascending (tp: per-plane
@@ -304,8 +311,7 @@ SFM_DEV void emit_keypoints(const SelectLds& L, int nsel, KpList kp, int b, int 
 // Both middle keys from the collected list at once: digit 2 (11 bits) of rank r1 in bucket b1
 // and of rank r2 in bucket b2 histogrammed in the two halves of s_h in one list pass, then
 // digit 3 (10 bits) likewise (as select_in_list twice, in half the passes).
-// The list's first kMedLdsCap keys live in LDS (ll), the rest in global memory (lp, same index).
-constexpr int kMedLdsCap = (kTopkLdsCap + kTieLdsCap) * 2;  // u32 keys over the sel + tie areas
+// The list's first L.med_cap keys live in LDS (ll), the rest in global memory (lp, same index).
 
 SFM_DEV void select_pair_in_list(const uint32_t* ll, const uint32_t* lp, int64_t m, uint32_t b1, uint32_t r1,
                                  uint32_t b2, uint32_t r2, const SelectLds& L, uint32_t* key1, uint32_t* key2,
@@ -314,7 +320,7 @@ SFM_DEV void select_pair_in_list(const uint32_t* ll, const uint32_t* lp, int64_t
   for (int i = tid; i < kHistBins; i += nt) L.h[i] = 0u;
   __syncthreads();
   for (int64_t i = tid; i < m; i += nt) {
-    const uint32_t k = i < kMedLdsCap ? ll[i] : lp[i];
+    const uint32_t k = i < L.med_cap ? ll[i] : lp[i];
     const bool in2 = (k >> 21) == b2;  // b1 == b2 is possible: both halves count the key
     hist_add(L.h, (k >> 10) & 0x7ffu, (k >> 21) == b1, agg);
     hist_add(L.h, 2048 + ((k >> 10) & 0x7ffu), in2, agg);
@@ -331,7 +337,7 @@ SFM_DEV void select_pair_in_list(const uint32_t* ll, const uint32_t* lp, int64_t
   for (int i = tid; i < 2048; i += nt) L.h[i] = 0u;
   __syncthreads();
   for (int64_t i = tid; i < m; i += nt) {
-    const uint32_t k = i < kMedLdsCap ? ll[i] : lp[i];
+    const uint32_t k = i < L.med_cap ? ll[i] : lp[i];
     hist_add(L.h, k & 0x3ffu, (k >> 10) == pre1, agg);
     hist_add(L.h, 1024 + (k & 0x3ffu), (k >> 10) == pre2, agg);
   }
@@ -346,7 +352,7 @@ SFM_DEV void select_pair_in_list(const uint32_t* ll, const uint32_t* lp, int64_t
 
 // np.median of the plane (NaiveSIFT.py:91): the keys of the two digit-1 buckets holding the
 // middle ranks (from the Harris histogram's select scan) are collected into a list whose
-// first kMedLdsCap keys stay in LDS (the top-k areas are free until the exact NMS), the rest
+// first L.med_cap keys stay in LDS (the top-k areas are free until the exact NMS), the rest
 // in `list`; then digits 2 and 3 are resolved from it.  Even n: float32 (v[n/2-1] + v[n/2]) / 2.
 // The plane is read with 16-B loads (8 per thread in flight) when it is 16-B aligned.
 SFM_DEV float exact_median(const float* Rp, int64_t n, const MedianState& s, uint32_t* list, const SelectLds& L,
@@ -361,11 +367,11 @@ SFM_DEV float exact_median(const float* Rp, int64_t n, const MedianState& s, uin
     const bool in = valid && (d == b1 || d == b2);
     const int slot = lds_wave_append(&L.cnt[0], in);
     if (in) {
-      if (slot < kMedLdsCap) ll[slot] = key;
+      if (slot < L.med_cap) ll[slot] = key;
       else list[slot] = key;
     }
   };
-  constexpr int U = 8;  // loads in flight per thread
+  constexpr int U = 4;  // loads in flight per thread (8 float4 loads cost k_select 10 VGPRs)
   if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(Rp) & 15) == 0) {
     const float4* R4 = reinterpret_cast<const float4*>(Rp);
     const int64_t n4 = n >> 2;
@@ -428,7 +434,7 @@ SFM_DEV int64_t exact_nms(const float* Rp, int H, int W, int kh, float med, uint
     // as below with 16-B loads: lane l of chunk ch owns columns x0 .. x0 + 3 (x0 = xb + 256 ch
     // + 4 l); the window's outer columns come from the neighbouring lanes' column maxima
     // (the chunk's edge lanes load the column beyond it)
-    constexpr int NCH = 1, RB = 4;
+    constexpr int NCH = 1, RB = 3;  // RB = 4: 90 VGPRs for the whole kernel, above its budget
     for (int y0 = wid * RB; y0 < H; y0 += nw * RB) {
       for (int xb = 0; xb < W; xb += 256 * NCH) {
         float4 c[RB + 2][NCH];
@@ -474,7 +480,7 @@ SFM_DEV int64_t exact_nms(const float* Rp, int H, int W, int kh, float med, uint
   } else if (kh == 1) {
     // RB output rows per wavefront iteration from RB + 2 image rows loaded once (every load
     // of the iteration in flight together)
-    constexpr int NCH = 2, RB = 4;
+    constexpr int NCH = 2, RB = 2;  // NCH = 2, RB = 4: 106 VGPRs
     for (int y0 = wid * RB; y0 < H; y0 += nw * RB) {
       for (int xb = 0; xb < W; xb += 64 * NCH) {
         float c[RB + 2][NCH], e[RB + 2][NCH];
@@ -539,7 +545,8 @@ SFM_DEV int64_t exact_nms(const float* Rp, int H, int W, int kh, float med, uint
   return C;
 }
 
-__global__ void __launch_bounds__(1024) k_select(SelectLevels g, int kcap, int k, int kh, int B, int abl) {
+__global__ void __launch_bounds__(1024) k_select(SelectLevels g, int kcap, int k, int kh, int B, int abl,
+                                                  int sel_cap) {
   // this workgroup's level and plane (levels are B workgroups each, level-major)
   const int li = (int)blockIdx.x / B;
   const SelectLevels::Level& lv = g.l[li];
@@ -556,11 +563,12 @@ __global__ void __launch_bounds__(1024) k_select(SelectLevels g, int kcap, int k
   __shared__ uint32_t s_cnt[2];
   SelectLds L;
   L.sel = reinterpret_cast<uint64_t*>(s_raw);
-  L.tie = L.sel + kTopkLdsCap;
+  L.tie = L.sel + sel_cap;
   L.h = reinterpret_cast<uint32_t*>(L.tie + kTieLdsCap);
   L.scan = L.h + kHistBins;
   L.out = s_out;
   L.cnt = s_cnt;
+  L.med_cap = (sel_cap + kTieLdsCap) * 2;
 
   const int tid = threadIdx.x;
   const int b = (int)blockIdx.x - li * B;
@@ -576,8 +584,10 @@ __global__ void __launch_bounds__(1024) k_select(SelectLevels g, int kcap, int k
     const int64_t C = (int64_t)cand_count[(int64_t)b * kCounterStride];  // certified NMS's candidates
     if (C >= (int64_t)k) {
       // SFMFEAT_SELECT_SUBSET=0 (A/B): always the full candidate list
-      if (!(abl & 32) && !topk_subset(cp, C, k, s.tsub, s.tnms, L)) topk_sorted(cp, C, k, tp, L, abl);
-      else if (abl & 32) topk_sorted(cp, C, k, tp, L, abl);
+      bool done = false;
+      if (!(abl & 32)) done = topk_subset(cp, C, k, s.tsub, s.tnms, L);
+      asm volatile("" ::: "memory");  // topk_sorted re-reads the keys: no 16 VGPRs held across
+      if (!done) topk_sorted(cp, C, k, tp, L, abl);
       if ((abl & 3) || ~(uint32_t)(L.sel[k - 1] >> 32) >= s.tcert) {  // k-th candidate above the median's bucket
         emit_keypoints(L, k, kp, b, kcap, H, W, hw);
         return;
@@ -600,9 +610,17 @@ __global__ void __launch_bounds__(1024) k_select(SelectLevels g, int kcap, int k
   emit_keypoints(L, kk, kp, b, kcap, H, W, hw);
 }
 
-size_t topk_lds_bytes() {
-  return (size_t)kTopkLdsCap * 8 + (size_t)kTieLdsCap * 8 + (size_t)kHistBins * 4 + 1024 * 4;
+static int select_sel_cap(int k) {
+  int p = kTopkDirect;
+  while (p < k) p <<= 1;
+  return p;
 }
+
+static size_t select_lds_bytes(int sel_cap) {
+  return (size_t)sel_cap * 8 + (size_t)kTieLdsCap * 8 + (size_t)kHistBins * 4 + 1024 * 4;
+}
+
+size_t topk_lds_bytes() { return select_lds_bytes(select_sel_cap(kTopkLdsCap)); }
 
 void launch_select_levels(const SelectLevels& g, int kcap, int k, int B, int ksize, hipStream_t st) {
   if (g.n < 1 || g.n > kSelectMaxLevels || B < 1) return;
@@ -611,7 +629,9 @@ void launch_select_levels(const SelectLevels& g, int kcap, int k, int B, int ksi
     const char* sb = getenv("SFMFEAT_SELECT_SUBSET");  // a correct variant (A/B): 0 = full list always
     return (e ? atoi(e) : 0) | ((sb && atoi(sb) == 0) ? 32 : 0);
   }();
-  hipLaunchKernelGGL(k_select, dim3(B * g.n), dim3(1024), topk_lds_bytes(), st, g, kcap, k, ksize / 2, B, abl);
+  const int sel_cap = select_sel_cap(k < 1 ? 1 : k);
+  hipLaunchKernelGGL(k_select, dim3(B * g.n), dim3(1024), select_lds_bytes(sel_cap), st, g, kcap, k, ksize / 2, B,
+                     abl, sel_cap);
 }
 
 void launch_select(const float* R, uint64_t* cand, const unsigned long long* cand_count, uint32_t* medlist,

@@ -60,23 +60,32 @@ def _device_asm(tmp_path) -> str:
                                     text=True).stdout for e in _device_elfs(tmp_path))
 
 
-def _kernel_lds(tmp_path) -> dict:
-    """Static LDS bytes per kernel symbol (.group_segment_fixed_size of the code objects'
-    AMDGPU metadata notes; the keys of each kernel's map print in sorted order, so a kernel's
-    size precedes its .name)."""
+def _kernel_meta(tmp_path) -> dict:
+    """Per kernel symbol: static LDS bytes, VGPRs and scratch bytes per lane, from the code
+    objects' AMDGPU metadata notes.  The keys of a kernel's map print in sorted order, starting
+    with .agpr_count; .vgpr_count follows .name, so a record closes at the next map's start."""
     readelf = os.path.join(LLVM, "llvm-readelf")
-    lds, g = {}, None
+    keys = {"group_segment_fixed_size": "lds", "vgpr_count": "vgpr", "private_segment_fixed_size": "scratch",
+            "name": "name"}
+    meta = {}
     for e in _device_elfs(tmp_path):
         notes = subprocess.run([readelf, "--notes", e], check=True, capture_output=True, text=True).stdout
-        for line in notes.splitlines():
-            m = re.search(r"\.group_segment_fixed_size:\s*(\d+)", line)
-            if m:
-                g = int(m.group(1))
-            m = re.search(r"^\s*\.name:\s*(\S+)", line)
-            if m and g is not None:
-                lds[m.group(1)] = g
-                g = None
-    return lds
+        cur = {}
+        for line in notes.splitlines() + ["  - .agpr_count: 0"]:
+            if re.match(r"^\s*-\s*\.agpr_count:", line):
+                if "name" in cur:
+                    meta[cur.pop("name")] = cur
+                cur = {}
+            for k, v in keys.items():
+                m = re.search(r"^\s*-?\s*\.%s:\s*(\S+)" % k, line)
+                if m and v not in cur:
+                    cur[v] = m.group(1) if v == "name" else int(m.group(1))
+    return meta
+
+
+def _kernel_lds(tmp_path) -> dict:
+    """Static LDS bytes per kernel symbol."""
+    return {k: v["lds"] for k, v in _kernel_meta(tmp_path).items()}
 
 
 def test_half_cu_sweep_fits_beside_one_harris_workgroup(tmp_path):
@@ -89,6 +98,29 @@ def test_half_cu_sweep_fits_beside_one_harris_workgroup(tmp_path):
     sweep3 = [v for k, v in lds.items() if k.startswith("_ZN3sfm12k_match_mfmaILi3ELi0E")]
     assert len(harris) == 1 and len(sweep3) == 1, (harris, sweep3)
     assert harris[0] + sweep3[0] <= 160 * 1024, f"k_harris {harris[0]} B + half-CU sweep {sweep3[0]} B > 160 KB"
+
+
+def test_select_workgroup_fits_beside_one_harris_workgroup(tmp_path):
+    """k_select (one 1,024-thread workgroup per plane, mostly waiting on loads) runs on the aux
+    stream while the other batch's k_harris holds the CUs.  Its LDS is sized per launch from k
+    (select.hip select_lds_bytes) and its VGPRs are budgeted so that one select workgroup and one
+    k_harris workgroup share a CU: LDS within 160 KB, and 4 select waves + 1 Harris wave per
+    SIMD within the 512-entry register file (allocation granule 8), with no scratch spills."""
+    meta = _kernel_meta(tmp_path)
+    harris = [v for k, v in meta.items() if k.startswith("_ZN3sfm8k_harrisILi7ELb1ELi0ELi0E")]
+    sel = [v for k, v in meta.items() if k.startswith("_ZN3sfm8k_selectE")]
+    assert len(harris) == 1 and len(sel) == 1, (harris, sel)
+    h, s = harris[0], sel[0]
+
+    def alloc(v):
+        return (v + 7) // 8 * 8
+
+    assert s["scratch"] == 0, f"k_select spills {s['scratch']} B per lane"
+    assert 4 * alloc(s["vgpr"]) + alloc(h["vgpr"]) <= 512, f"k_select {s['vgpr']} VGPRs x 4 + k_harris {h['vgpr']} > 512"
+    k = 2500  # BASELINE's k: sel area next_pow2(k) keys, ties 2048, 4096-bin histogram, 1024 scan words
+    sel_cap = max(2048, 1 << (k - 1).bit_length())
+    dyn = sel_cap * 8 + 2048 * 8 + 4096 * 4 + 1024 * 4
+    assert s["lds"] + dyn + h["lds"] <= 160 * 1024, f"k_select {s['lds'] + dyn} B + k_harris {h['lds']} B > 160 KB"
 
 
 def test_no_packed_fma_with_src1_high_half_select(tmp_path):

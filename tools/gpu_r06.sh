@@ -18,7 +18,7 @@ step() {  # step NAME SECONDS CMD...
   echo "[$(date +%T)] $name"
   timeout -k 10 "$to" "$@" > "$O/${T}_$name.out" 2> "$O/${T}_$name.err"
   local rc=$?
-  [ $rc -eq 0 ] || { echo "$name rc=$rc"; tail -30 "$O/${T}_$name.err" "$O/${T}_$name.out"; exit $rc; }
+  [ $rc -eq 0 ] || { echo "$name rc=$rc"; tail -n 30 "$O/${T}_$name.err" "$O/${T}_$name.out"; exit $rc; }
 }
 for s in ${STEPS:-tests smoke bench trace}; do
   case $s in
