@@ -9,7 +9,7 @@
 //                      the same top-k over those candidates;
 //   edge filter      : h <= y < H-h, h <= x < W-h (h = feature_width // 2), applied AFTER
 //                      top-k; keys stay in ascending key order (confidence descending).
-// Up to kTopkDirect candidates are sorted directly in LDS; beyond that a block radix select
+// Up to max(kTopkDirect, next_pow2(k)) candidates are sorted directly in LDS; beyond that a block radix select
 // on the confidence half of the key finds the k-th key (ties on confidence resolved by
 // raster index, exactly), and only the selected k keys are sorted.
 //
@@ -129,6 +129,7 @@ struct SelectLds {
   uint32_t* out;   // 2
   uint32_t* cnt;   // 2
   int med_cap;     // u32 median-list keys held over the sel + tie areas
+  int sel_cap;     // keys the sel area holds (>= kTopkDirect): lists up to it are sorted whole
 };
 
 // The kk (>= 1) smallest of the C keys cp[0..C) into L.sel[0..kk), ascending (tp: per-plane
@@ -139,7 +140,9 @@ struct SelectLds {
 // SFMFEAT_SELECT_SUBSET=0): no subset fast path (topk_subset)
 SFM_DEV void topk_sorted(const uint64_t* cp, int64_t C, int kk, uint64_t* tp, const SelectLds& L, int abl = 0) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  if (C <= kTopkDirect) {
+  // up to sel_cap keys: sorted whole (for k > kTopkDirect the k-key sort below runs over the
+  // same next_pow2 slots, so the radix select would only add to it)
+  if (C <= L.sel_cap) {
     for (int i = tid; i < C; i += nt) L.sel[i] = cp[i];
     __syncthreads();
     sort_keys_u64(L.sel, (int)C);
@@ -227,18 +230,18 @@ SFM_DEV int lds_wave_append(uint32_t* counter, bool pred) {
   return pred ? (int)(base + (uint32_t)__popcll(lower)) : -1;
 }
 
-// Certified planes with more than kTopkDirect candidates: the candidates at or above a higher
+// Certified planes with more than L.sel_cap candidates: the candidates at or above a higher
 // threshold tsub[t] (MedianState) — the 3 vmin / 8-th or vmin / 2-th largest value's bucket,
-// about 1-3k keys at vmin = 128 k instead of 3-7k — when at least kk (and at most kTopkDirect)
-// of them exist.  Every candidate outside that subset lies below its threshold, i.e. below
-// each of its members, so its kk best keys are the whole list's kk best (the caller's
-// certification test then applies unchanged).  Sorted whole in L.sel; true when taken, false
+// about 1-3k keys at vmin = 128 k instead of 3-7k — when at least kk (and at most L.sel_cap:
+// kTopkDirect, or next_pow2(k) above it) of them exist.  Every candidate outside that subset
+// lies below its threshold, i.e. below each of its members, so its kk best keys are the whole
+// list's kk best (the caller's certification test then applies unchanged).  Sorted whole in L.sel; true when taken, false
 // (nothing written) when neither subset fits: the caller runs the full top-k.
 SFM_DEV bool topk_subset(const uint64_t* cp, int64_t C, int kk, const uint32_t (&tsub)[2], uint32_t tnms,
                          const SelectLds& L) {
   const int tid = threadIdx.x, nt = blockDim.x;
   // (tsub[0] >= tsub[1] >= tnms: when tsub[0] == tnms both subsets are the whole list)
-  if (C <= kTopkDirect || C > (int64_t)kRegKeys * nt || tsub[0] <= tnms) return false;
+  if (C <= L.sel_cap || C > (int64_t)kRegKeys * nt || tsub[0] <= tnms) return false;
   uint64_t kr[kRegKeys];
 #pragma unroll
   for (int j = 0; j < kRegKeys; ++j) {
@@ -262,8 +265,8 @@ SFM_DEV bool topk_subset(const uint64_t* cp, int64_t C, int kk, const uint32_t (
   }
   __syncthreads();
   const uint32_t n0 = L.cnt[0], n1 = L.cnt[1];
-  const int t = (n0 >= (uint32_t)kk && n0 <= (uint32_t)kTopkDirect) ? 0
-              : (tsub[1] > tnms && n1 >= (uint32_t)kk && n1 <= (uint32_t)kTopkDirect) ? 1 : -1;
+  const uint32_t cap = (uint32_t)L.sel_cap;
+  const int t = (n0 >= (uint32_t)kk && n0 <= cap) ? 0 : (tsub[1] > tnms && n1 >= (uint32_t)kk && n1 <= cap) ? 1 : -1;
   if (t < 0) return false;  // (uniform)
   const uint32_t ht = t == 0 ? h0 : h1;
   __syncthreads();
@@ -569,6 +572,7 @@ __global__ void __launch_bounds__(1024) k_select(SelectLevels g, int kcap, int k
   L.out = s_out;
   L.cnt = s_cnt;
   L.med_cap = (sel_cap + kTieLdsCap) * 2;
+  L.sel_cap = sel_cap;
 
   const int tid = threadIdx.x;
   const int b = (int)blockIdx.x - li * B;
