@@ -287,6 +287,44 @@ int32_t sfm_gate_create(int32_t device, sfm_gate** out);
 int32_t sfm_gate_destroy(sfm_gate* gate);
 int32_t sfm_ctx_set_gate(sfm_ctx* ctx, sfm_gate* gate);
 
+/* ---------------- multi-GPU exchange over RCCL (SURVEY.md §8b "sfm_dist_*", §8e) ----------
+ * The reference fans the extractor and matcher out over 8 threads of one process
+ * (Runner.py:183-191, 336-355); sharded over GPUs (one process per GPU, frames in contiguous
+ * shards), the only data exchanged is the slot table the match schedule needs: the halo slot
+ * of the consecutive schedule and, for configs[3], each chunk's slots on every rank.  These
+ * calls move exactly that over RCCL without torch: a host in any language creates one
+ * communicator per rank (the 128-byte id made by one rank and handed to the others over any
+ * channel), then enqueues the exchange on its stream next to sfm_extract_batch_dev /
+ * sfm_match_pairs_dev.  RCCL is loaded at run time (the copy already in the process, e.g.
+ * PyTorch's, else librccl.so.1 from the library path): without it every call returns
+ * SFM_EDEVICE and the rest of the library is unaffected.  One device per rank (RCCL does not
+ * allow two ranks of one communicator on the same GPU).  Slot-table layout as
+ * sfm_extract_batch_dev writes it: xy [slot][cap][2] int32, desc [slot][cap][128] float32,
+ * count [slot] int32.  Errors: SFM_EINVAL (arguments), SFM_EDEVICE (RCCL / HIP; text via
+ * sfm_dist_last_error, which takes NULL for failures before a communicator exists). */
+#define SFM_DIST_ID_BYTES 128
+typedef struct sfm_dist sfm_dist;
+int32_t sfm_dist_unique_id(uint8_t* id /* [SFM_DIST_ID_BYTES] */);
+/* Collective over the `world` ranks: every rank calls it with the same id (blocks until all
+ * have joined). */
+int32_t sfm_dist_create(int32_t device, int32_t rank, int32_t world, const uint8_t* id, sfm_dist** out);
+int32_t sfm_dist_destroy(sfm_dist* d);
+const char* sfm_dist_last_error(const sfm_dist* d);
+int32_t sfm_dist_rank(const sfm_dist* d, int32_t* rank, int32_t* world);
+/* configs[3]'s chunk gather (distributed.py allgather_chunk): every rank's bc slots
+ * (src_*) land at table slots [base + r * bc, base + (r + 1) * bc) of every rank r, all three
+ * fields in one grouped RCCL launch on `stream`.  In place (no copy of the own slots) when
+ * src_* point at the table's own slots base + rank * bc. */
+int32_t sfm_dist_allgather_slots_dev(sfm_dist* d, int32_t bc, int32_t cap, const int32_t* src_xy,
+                                     const float* src_desc, const int32_t* src_count, int32_t* tab_xy,
+                                     float* tab_desc, int32_t* tab_count, int64_t base, void* stream);
+/* The consecutive schedule's halo (distributed.py halo_exchange): rank r sends its slot
+ * (src_*, one slot) to rank r - 1 and receives rank r + 1's into dst_* (one slot); the first
+ * rank only receives, the last only sends, a single rank does nothing. */
+int32_t sfm_dist_halo_dev(sfm_dist* d, int32_t cap, const int32_t* src_xy, const float* src_desc,
+                          const int32_t* src_count, int32_t* dst_xy, float* dst_desc, int32_t* dst_count,
+                          void* stream);
+
 /* ---------------- stage profiling (bench.py's live roofline numbers) ----------------
  * When enabled, every stage's launches are bracketed by HIP events on the launch
  * stream; sfm_profile_read synchronises them and returns the accumulated device time

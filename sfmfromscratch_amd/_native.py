@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import threading
 
 import numpy as np
@@ -79,6 +80,14 @@ SIGNATURES = {
     "sfm_debug_match_stamps": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_int64]),
     "sfm_debug_select_stats": (ctypes.c_int32, [_vp, _i32p, _i32p]),
     "sfm_copy_wg": (ctypes.c_int32, [_vp, _vp, ctypes.c_int64, ctypes.c_int32, _vp]),
+    "sfm_dist_unique_id": (ctypes.c_int32, [_u8p]),
+    "sfm_dist_create": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _u8p, ctypes.POINTER(_vp)]),
+    "sfm_dist_destroy": (ctypes.c_int32, [_vp]),
+    "sfm_dist_last_error": (ctypes.c_char_p, [_vp]),
+    "sfm_dist_rank": (ctypes.c_int32, [_vp, _i32p, _i32p]),
+    "sfm_dist_allgather_slots_dev": (ctypes.c_int32, [_vp, ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp,
+                                                      _vp, ctypes.c_int64, _vp]),
+    "sfm_dist_halo_dev": (ctypes.c_int32, [_vp, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
 
     "sfm_debug_copy_level": (ctypes.c_int32, [_vp, ctypes.c_int32, ctypes.c_int32, _vp, _vp]),
     "sfm_debug_atan2": (ctypes.c_int32, [ctypes.c_int32, _fp, _fp, _fp, ctypes.c_int64]),
@@ -112,6 +121,17 @@ def _preload_torch_hip_runtime():
             except OSError:
                 pass
             return
+
+
+def _preload_torch_rccl():
+    """sfm_dist_* bind the librccl.so.1 already in the process: when PyTorch is installed its
+    copy must be that one (one collective runtime per process), so torch is imported first and
+    loads it in its own order.  (Loading torch's librccl.so by path before `import torch`
+    aborts the interpreter at exit: a double free in the libraries' teardown.)  Without torch
+    the library path's RCCL is used."""
+    import importlib.util
+    if "torch" not in sys.modules and importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401
 
 
 def load_library(path: str | None = None):
@@ -426,6 +446,85 @@ class Gate:
     def close(self):
         if getattr(self, "handle", None) is not None and self.handle.value:
             self.lib.sfm_gate_destroy(self.handle)
+            self.handle = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Dist:
+    """sfm_dist: one rank's RCCL communicator for the sharded jobs' exchange (include/sfmfeat.h
+    sfm_dist_*): the consecutive schedule's halo slot and configs[3]'s per-chunk
+    slot gather, enqueued on a stream, without torch.distributed.  One rank makes the id
+    (`unique_id`) and hands it to the others over any channel; `from_process_group` uses a
+    torch.distributed group's broadcast for that."""
+
+    def __init__(self, device: int, rank: int, world: int, uid: bytes):
+        self.lib = load_library()
+        _preload_torch_rccl()
+        if len(uid) != 128:
+            raise ValueError("the RCCL unique id is 128 bytes")
+        ub = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        h = _vp()
+        rc = self.lib.sfm_dist_create(int(device), int(rank), int(world), ub, ctypes.byref(h))
+        if rc != _abi.SFM_OK:
+            msg = (self.lib.sfm_dist_last_error(None) or b"").decode()
+            if rc == _abi.SFM_EINVAL:
+                raise ValueError(msg)
+            raise RuntimeError(f"sfm_dist_create: {msg}")
+        self.handle, self.device, self.rank, self.world = h, int(device), int(rank), int(world)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = load_library()
+        _preload_torch_rccl()
+        buf = (ctypes.c_uint8 * 128)()
+        if lib.sfm_dist_unique_id(buf) != _abi.SFM_OK:
+            raise RuntimeError(f"sfm_dist_unique_id: {(lib.sfm_dist_last_error(None) or b'').decode()}")
+        return bytes(buf)
+
+    @classmethod
+    def from_process_group(cls, dist, device: int, group=None) -> "Dist":
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        box = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=group)
+        return cls(device, rank, world, box[0])
+
+    def _check(self, rc: int):
+        if rc == _abi.SFM_OK:
+            return
+        msg = (self.lib.sfm_dist_last_error(self.handle) or b"").decode()
+        if rc == _abi.SFM_EINVAL:
+            raise ValueError(msg)
+        raise RuntimeError(f"sfm_dist: {msg}")
+
+    def allgather_slots(self, table, base: int, src, bc: int, stream: int = 0):
+        """Every rank's src slots [0, bc) -> table slots [base + r * bc, ...) (pipeline.SlotTable
+        fields; in place when src is the table's own slots base + rank * bc)."""
+        cap = int(table.xy.shape[1])
+        if int(src.xy.shape[1]) != cap or base + self.world * bc > int(table.xy.shape[0]) or bc > int(src.xy.shape[0]):
+            raise ValueError("allgather_slots: slot shapes do not fit")
+        self._check(self.lib.sfm_dist_allgather_slots_dev(
+            self.handle, int(bc), cap, src.xy.data_ptr(), src.desc.data_ptr(), src.count.data_ptr(),
+            table.xy.data_ptr(), table.desc.data_ptr(), table.count.data_ptr(), int(base), stream or None))
+
+    def halo(self, slots, n_local: int, stream: int = 0):
+        """distributed.halo_exchange's move: rank r + 1's slot 0 into this rank's slot n_local."""
+        cap = int(slots.xy.shape[1])
+        recvs = self.rank < self.world - 1
+        if recvs and n_local >= int(slots.xy.shape[0]):
+            raise ValueError("halo: the slot table has no slot n_local")
+        dst = (slots.xy[n_local].data_ptr(), slots.desc[n_local].data_ptr(), slots.count[n_local:].data_ptr()) \
+            if recvs else (None, None, None)
+        self._check(self.lib.sfm_dist_halo_dev(self.handle, cap, slots.xy.data_ptr(), slots.desc.data_ptr(),
+                                               slots.count.data_ptr(), *dst, stream or None))
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            self.lib.sfm_dist_destroy(self.handle)
             self.handle = _vp()
 
     def __del__(self):
