@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 GPU evidence, one gpurun call: STEPS selects what runs (space-separated):
 #   tests   the GPU suite          smoke   __graft_entry__.smoke()
-#   bench   the driver's command (python bench.py) BENCH_N times
+#   bench   the driver's command (python bench.py --gpus 1 --steps 20 --warmup 5) BENCH_N times
 #   trace   rocprofv3 --kernel-trace --stats of the driver's command + tools/trace_roofline.py
 #   c3 c4 c5  the other BASELINE configurations        sq  one SQ counter pass
 #   pmc     FETCH_SIZE / WRITE_SIZE passes (HBM traffic per kernel)
@@ -30,7 +30,7 @@ for s in ${STEPS:-tests smoke bench trace}; do
       tail -1 $O/${T}_smoke.out ;;
     bench)
       for i in $(seq 1 ${BENCH_N:-1}); do
-        step bench_$i 300 python bench.py ${BENCH_ARGS:-}
+        step bench_$i 300 python bench.py ${BENCH_ARGS:---gpus 1 --steps 20 --warmup 5}
         python -c "import json;d=json.load(open('$O/${T}_bench_$i.out'));r=d['roofline'];print('c2', d['value'], d['ms_per_step'], r['frac'], r['ms_per_step'], r['launch_sum'])"
       done ;;
     trace)
