@@ -1,7 +1,8 @@
 """Harris alone, per pyramid level of the configs[1] step: the mean duration of one k_harris<7>
 launch over 32 planes of each P-oct level size (sfm_debug_time_harris, abl 0: the product kernel
 on synthetic planes, no other work on the GPU), and their sum = Harris per step alone.
-usage: python tools/harris_alone.py [iters] [lib.so]"""
+usage: python tools/harris_alone.py [iters] [lib.so] [abl]  (abl != 0: the diagnostic build's timing
+ablations, e.g. 1 = no digit histogram)"""
 import os
 import sys
 
@@ -17,11 +18,12 @@ L = ctypes.CDLL(sys.argv[2] if len(sys.argv) > 2 else _native.LIB_PATH)  # any b
 f = L.sfm_debug_time_harris
 f.restype = ctypes.c_float
 f.argtypes = [ctypes.c_int32] * 6
-f(0, 0, 32, 1080, 1920, 3)  # warm-up
+abl = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+f(0, abl, 32, 1080, 1920, 3)  # warm-up
 tot, px = 0.0, 0
 for lvl in range(4):
     H, W = 1080 >> lvl, 1920 >> lvl
-    ms = f(0, 0, 32, H, W, iters)
+    ms = f(0, abl, 32, H, W, iters)
     tot += ms
     px += 32 * H * W
     print(f"L{lvl} {H}x{W} x32: {ms * 1e3:8.1f} us", flush=True)
