@@ -574,26 +574,19 @@ def main():
                    "host_step_submit_ms_max": round(max(host_ms), 3) if host_ms else None,
                    "host_step_submit_ms_median": round(float(np.median(host_ms)), 3) if host_ms else None}
 
-    # the describe floor's keypoint counts: a host-path extraction (PCIe copies, the GPU
-    # mostly idle), so after the timed region rather than between the profile pass and the
-    # warm-up, where it would let the GPU's clocks drop right before timing
-    if stages and "describe" in stages:
-        lvl_kp = level_keypoints()
-        if lvl_kp is not None:
-            fl_ms, ops = describe_floor(lvl_kp, nprof)
-            d = stages["describe"]
-            d.update({"bound": "valu", "achieved": round(ops / (prof_all["describe"][0] / 1e3) / 1e12, 3),
-                      "unit": "T lane-op/s", "floor_ms_per_step": round(fl_ms / nprof, 4),
-                      "frac": round(fl_ms / prof_all["describe"][0], 4),
-                      "keypoints_per_level": [int(v) for v in lvl_kp],
-                      "note": "modelled lane-ops per keypoint (bench.describe_ops) / 39.3 T lane-op/s"})
-
     # the same K steps again with one batch submitted every step (the pre-round-5 workload): the
     # line reports its rate beside `value` (alternating batches) as the cost of never re-reading
-    # the previous step's frames
+    # the previous step's frames.  Right after the timed region and after its own warm-up, before
+    # the host-path extraction below idles the GPU (a 20-step pass started on dropped clocks
+    # read 10 % slow)
     same_value = None
     if batches is not None and len(batches) > 1:
         same_batch[0] = True
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        pipe.n = 0
+        run_steps(args.warmup)  # untimed, like the headline's warm-up (clocks, caches, lanes)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -612,6 +605,20 @@ def main():
             el = float(t.item())
         same_value = world * B * args.steps / el
         same_batch[0] = False
+
+    # the describe floor's keypoint counts: a host-path extraction (PCIe copies, the GPU
+    # mostly idle), so after the timed region rather than between the profile pass and the
+    # warm-up, where it would let the GPU's clocks drop right before timing
+    if stages and "describe" in stages:
+        lvl_kp = level_keypoints()
+        if lvl_kp is not None:
+            fl_ms, ops = describe_floor(lvl_kp, nprof)
+            d = stages["describe"]
+            d.update({"bound": "valu", "achieved": round(ops / (prof_all["describe"][0] / 1e3) / 1e12, 3),
+                      "unit": "T lane-op/s", "floor_ms_per_step": round(fl_ms / nprof, 4),
+                      "frac": round(fl_ms / prof_all["describe"][0], 4),
+                      "keypoints_per_level": [int(v) for v in lvl_kp],
+                      "note": "modelled lane-ops per keypoint (bench.describe_ops) / 39.3 T lane-op/s"})
 
     images = world * B * args.steps
     value = images / elapsed
