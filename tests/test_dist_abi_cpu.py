@@ -43,3 +43,38 @@ def test_unique_ids_are_128_distinct_bytes():
     pytest.importorskip("torch")  # the RCCL bound here is PyTorch's copy (or the system's)
     a, b = _native.Dist.unique_id(), _native.Dist.unique_id()
     assert len(a) == len(b) == 128 and a != b
+
+
+def test_integration_c_snippet_compiles_against_the_header(tmp_path):
+    """INTEGRATION.md §3's C use of the exchange beside the batch calls (one rank's chunk:
+    extract into the table's own slots, gather in place, match) compiles against
+    include/sfmfeat.h with -Werror: the documented binding matches the declared signatures."""
+    src = tmp_path / "rank.c"
+    src.write_text(r'''
+#include <stdint.h>
+#include "sfmfeat.h"
+int rank_chunk(sfm_ctx* ctx, const float* frames, int32_t B, int32_t H, int32_t W, int32_t rank,
+               int32_t world, int32_t device, int64_t base, int64_t cap, int32_t n_slots, int32_t* xy,
+               float* desc, int32_t* count, const int32_t* pairs, int32_t P, int32_t* m, float* conf,
+               int32_t* nm, void* stream) {
+  uint8_t id[SFM_DIST_ID_BYTES];
+  if (rank == 0 && sfm_dist_unique_id(id) != SFM_OK) return -1;   /* then broadcast id */
+  sfm_dist* d = 0;
+  if (sfm_dist_create(device, rank, world, id, &d) != SFM_OK) return -2;
+  const int64_t own = base + (int64_t)rank * B;
+  int rc = sfm_extract_batch_dev(ctx, frames, B, H, W, xy + own * cap * 2, desc + own * cap * 128,
+                                 count + own, cap, stream);
+  if (rc == SFM_OK)
+    rc = sfm_dist_allgather_slots_dev(d, B, (int32_t)cap, xy + own * cap * 2, desc + own * cap * 128,
+                                      count + own, xy, desc, count, base, stream);
+  if (rc == SFM_OK)
+    rc = sfm_match_pairs_dev(ctx, desc, count, n_slots, cap, pairs, P, 0.85f, m, conf, nm, stream);
+  int32_t r = -1, w = -1;
+  sfm_dist_rank(d, &r, &w);
+  if (rc != SFM_OK) (void)sfm_dist_last_error(d);
+  sfm_dist_destroy(d);
+  return rc;
+}
+''')
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-c", "-I", os.path.join(ROOT, "include"), str(src),
+                    "-o", str(tmp_path / "rank.o")], check=True)
