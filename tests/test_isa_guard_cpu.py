@@ -17,6 +17,7 @@ import os
 import re
 import shutil
 import subprocess
+import sys
 
 import pytest
 
@@ -136,3 +137,22 @@ def test_no_packed_fma_with_src1_high_half_select(tmp_path):
             if op in line and pat.search(line):
                 bad.append(f"{kernel}: {line.split('//')[0].strip()}")
     assert not bad, f"{len(bad)} hazardous instructions, e.g. {bad[:3]}"
+
+
+def test_harris_window_at_its_fma_floor_and_non_window_valu_bounded():
+    """The shipped product Harris kernel (k_harris<7, true, 0, 0>) from the built library's ISA
+    (tools/isa_phases.py, static counts over the tile loop, interior and border branches both
+    counted): the window is exactly the 49-tap fmaf contract's 16 px x 147 = 2352 fmas per
+    tile-thread, and the instructions around it stay at most 1,000 per tile-wave (977 at the end
+    of round 6; 607 on the interior path alone, profiles/r06_harris_isa_phases_interior.txt), so
+    a compiler or source change that brings back round 5's overhead (the LDS tap reads, the
+    scalar R epilogue: 918 on the interior path) fails here."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_phases as ip
+    if not os.path.exists(LIB) or not os.path.exists(os.path.join(LLVM, "llvm-objdump")):
+        pytest.skip("library or ROCm LLVM tools not available")
+    _, ins = ip.kernel_body(ip.disassemble(LIB), "k_harrisILi7ELb1ELi0ELi0E")
+    cnt, _, _, _, _, win, sc = ip.phase_counts(ins)
+    assert 2 * win + sc == 16 * 147, (win, sc)
+    non_window = sum(cnt.values()) - cnt["window fmas"]
+    assert non_window <= 1000, f"{non_window} non-window VALU per tile-wave"
